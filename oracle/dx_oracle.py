@@ -1,0 +1,278 @@
+"""CPU oracle: scalar NumPy restatement of the reference hot path.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the
+checker / the timed CPU baseline.  The product (the HIP library behind
+``include/dxrl.h``) never calls it and has no CPU fallback.
+
+Parity: PINNED.  ``tests/test_oracle_golden.py`` checks this restatement
+bit-exactly (obs, flags, contacts, object position, learner state) and to
+1e-12 relative on rewards (np.exp vs libm differ by <= 1 ulp) against the
+fixtures in ``tests/golden/`` that ``tests/golden/gen_golden.py`` captured
+from the reference itself.
+
+Each function follows the reference op by op under NumPy 2 / NEP 50 scalar
+promotion:
+
+* ``OracleEnv.reset``  <- envs/manipulation_env.py:124-182, experiments/config.py:44-113
+* ``OracleEnv.step``   <- envs/manipulation_env.py:184-252
+* ``_contacts``        <- envs/manipulation_env.py:285-310
+* ``_dense_reward``    <- rewards/reward_shaping.py:50-187
+* ``_sparse_reward``   <- rewards/reward_shaping.py:205-242
+* ``OracleSimpleLearner`` <- policies/simple_learner.py:49-99
+* ``oracle_run_episode``  <- training/episode_utils.py:13-55
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+f32 = np.float32
+F, J, D = 5, 3, 15
+LO = (-0.2, -0.2, 0.0)   # manipulation_env.py:119 workspace bounds
+HI = (0.2, 0.2, 0.3)
+GZ = -9.81 * 0.01        # manipulation_env.py:211-212 (f64)
+
+
+@dataclass
+class OracleCurriculum:
+    """experiments/config.py:17-42 (only what reset/step read)."""
+    object_size: float = 0.05
+    object_mass: float = 0.1
+    friction_coefficient: float = 0.5
+    size_range: Optional[Sequence[float]] = None
+    mass_range: Optional[Sequence[float]] = None
+    friction_range: Optional[Sequence[float]] = None
+    spawn_x_range: Sequence[float] = (-0.1, 0.1)
+    spawn_y_range: Sequence[float] = (-0.1, 0.1)
+    spawn_z_range: Sequence[float] = (0.05, 0.2)
+    # NEP 50: a numpy.float64 friction (scheduler interpolation) makes
+    # `ov *= damping` an f64 multiply instead of an f32 one.
+    friction_is_np_float64: bool = False
+
+    @classmethod
+    def from_record(cls, r: dict) -> "OracleCurriculum":
+        return cls(object_size=r["object_size"], object_mass=r["object_mass"],
+                   friction_coefficient=r["friction_coefficient"],
+                   size_range=r.get("object_size_range"), mass_range=r.get("object_mass_range"),
+                   friction_range=r.get("friction_range"),
+                   spawn_x_range=r["spawn_x_range"], spawn_y_range=r["spawn_y_range"],
+                   spawn_z_range=r["spawn_z_range"],
+                   friction_is_np_float64="friction_coefficient" in r.get("_float64_scalars", []))
+
+
+def reset_draws(rng: np.random.Generator, cur: OracleCurriculum, first: bool) -> np.ndarray:
+    """The 21 draw slots reset() consumes, in the reference's order
+    (manipulation_env.py:143-161); NaN where no draw happens."""
+    jp = rng.uniform(low=-0.1, high=0.1, size=(D,))
+    size = mass = fric = math.nan
+    if cur.size_range is not None:
+        size = float(rng.uniform(cur.size_range[0], cur.size_range[1]))
+    if cur.mass_range is not None:
+        mass = float(rng.uniform(cur.mass_range[0], cur.mass_range[1]))
+    if cur.friction_range is not None:
+        fric = float(rng.uniform(cur.friction_range[0], cur.friction_range[1]))
+    spawn = [math.nan] * 3
+    if first:
+        spawn = [float(rng.uniform(*cur.spawn_x_range)), float(rng.uniform(*cur.spawn_y_range)),
+                 float(rng.uniform(*cur.spawn_z_range))]
+    return np.concatenate([jp, [size, mass, fric], spawn])
+
+
+def _clip(x, lo, hi):
+    return lo if x < lo else (hi if x > hi else x)
+
+
+@dataclass
+class OracleEnv:
+    """One DexterousManipulationEnv, scalar state in exact reference dtypes."""
+    cur: OracleCurriculum = field(default_factory=OracleCurriculum)
+    dense: bool = True
+    max_episode_steps: int = 200
+    weights: Sequence[float] = (1.0, 0.5, 0.3, 0.2)  # reward_shaping.py:22-25
+    object_position: Optional[Sequence[float]] = None  # constructor arg (:28)
+
+    def __post_init__(self):
+        self.jp = [f32(0)] * D
+        self.jv = [f32(0)] * D
+        self.op = None if self.object_position is None else [float(v) for v in self.object_position]
+        self.op_is_f32 = True
+        self.ov = [f32(0)] * 3
+        self.contacts = [0] * F
+        self.prev = None
+        self.t = 0
+        self.size = self.mass = self.fric = None
+        self.last_components = None
+
+    # -- A2 ---------------------------------------------------------------
+    def reset(self, draws: np.ndarray):
+        self.jp = [f32(v) for v in draws[:D]]
+        self.jv = [f32(0)] * D
+        c = self.cur
+        self.size = draws[D] if c.size_range is not None else c.object_size
+        self.mass = draws[D + 1] if c.mass_range is not None else c.object_mass
+        self.fric = draws[D + 2] if c.friction_range is not None else c.friction_coefficient
+        if self.op is None:
+            src = draws[D + 3:D + 6]
+        else:
+            src = self.op
+        self.op = [float(f32(v)) for v in src]  # np.array(..., dtype=float32)
+        self.op_is_f32 = True
+        self.ov = [f32(0)] * 3
+        self.t = 0
+        self._contacts()
+        self.prev = None
+        return self.obs()
+
+    # -- A4 ---------------------------------------------------------------
+    def _contacts(self):
+        thr = self.size * 1.5
+        self.tips, self.dist = [], []
+        for f in range(F):
+            s = f32(f32(self.jp[3 * f] + self.jp[3 * f + 1]) + self.jp[3 * f + 2])
+            tip = float(f32(s * f32(0.1)))
+            dx, dy, dz = tip - self.op[0], tip - self.op[1], tip - self.op[2]
+            d = math.sqrt((dx * dx + dy * dy) + dz * dz)
+            self.tips.append(tip)
+            self.dist.append(d)
+        self.contacts = [1 if d < thr else 0 for d in self.dist]
+
+    # -- A5 / A6 -----------------------------------------------------------
+    def _dense_reward(self):
+        dist = float(np.exp(-5.0 * min(self.dist)))
+        n = sum(self.contacts)
+        con = n / F
+        cl = []
+        for f in range(F):
+            acc = f32(0)
+            for j in range(J):
+                v = self.jp[3 * f + j]
+                if v < 0:
+                    acc = f32(acc + v)
+            cl.append(f32(-acc))
+        s = f32(0)
+        for v in cl:
+            s = f32(s + v)
+        avg = f32(s / f32(F))
+        clo = float(_clip(f32(avg / f32(F)), f32(0), f32(1)))
+        if self.prev is None:
+            self.prev = list(self.contacts)
+            st = 0.0
+        else:
+            ch = f32(0)
+            for a, b in zip(self.contacts, self.prev):
+                ch = f32(ch + f32(abs(a - b)))
+            st = float(_clip(f32(f32(1) - f32(ch / f32(F))), f32(0), f32(1)))
+            self.prev = list(self.contacts)
+        w = self.weights
+        total = w[0] * dist + w[1] * con + w[2] * clo + w[3] * st
+        return total, (dist, con, clo, st)
+
+    def _sparse_reward(self):
+        return (1.0 if sum(self.contacts) >= 3 else -0.01), (0.0, 0.0, 0.0, 0.0)
+
+    # -- A3 + A7 -----------------------------------------------------------
+    def step(self, action):
+        a = [_clip(f32(x), f32(-1), f32(1)) for x in action]
+        self.jv = [f32(f32(f32(0.9) * v) + f32(f32(0.1) * x)) for v, x in zip(self.jv, a)]
+        self.jp = [_clip(f32(p + f32(v * f32(0.01))), f32(-1), f32(1)) for p, v in zip(self.jp, self.jv)]
+        damp = 1.0 - (self.fric * 0.1 * 0.01)
+        if self.cur.friction_is_np_float64:
+            self.ov = [f32(float(v) * damp) for v in self.ov]
+        else:
+            self.ov = [f32(v * f32(damp)) for v in self.ov]
+        self.ov = [f32(float(v) + g) for v, g in zip(self.ov, (0.0, 0.0, GZ))]
+        inc = [f32(v * f32(0.01)) for v in self.ov]
+        if self.op_is_f32:
+            op = [float(f32(f32(p) + i)) for p, i in zip(self.op, inc)]
+        else:
+            op = [p + float(i) for p, i in zip(self.op, inc)]
+        self.op = [min(max(p, lo), hi) for p, lo, hi in zip(op, LO, HI)]
+        self.op_is_f32 = False
+        for i in range(3):
+            if (self.op[i] <= LO[i] and self.ov[i] < 0) or (self.op[i] >= HI[i] and self.ov[i] > 0):
+                self.ov[i] = f32(0)
+        self._contacts()
+        reward, comps = self._dense_reward() if self.dense else self._sparse_reward()
+        self.last_components = comps
+        n = sum(self.contacts)
+        terminated = n >= 3
+        truncated = self.t >= self.max_episode_steps
+        self.t += 1
+        return self.obs(), reward, terminated, truncated
+
+    def obs(self):
+        o = np.empty(45, np.float32)
+        o[0:15] = self.jp
+        o[15:30] = self.jv
+        o[30:33] = self.op
+        o[33:37] = (1.0, 0.0, 0.0, 0.0)
+        o[37:40] = self.ov
+        o[40:45] = self.contacts
+        return o
+
+    @property
+    def num_contacts(self):
+        return sum(self.contacts)
+
+
+class OracleSimpleLearner:
+    """policies/simple_learner.py:13-99 driven by a tape of legacy-MT19937
+    gauss values (np.random.normal(0, s) == 0 + s * gauss)."""
+
+    def __init__(self, gauss: np.ndarray, learning_rate=0.01, exploration_noise=0.3, clip_range=0.5):
+        self.g = gauss
+        self.cur = 0
+        self.lr, self.noise, self.clip = learning_rate, exploration_noise, clip_range
+        self.mean = [f32(0)] * D
+        self.best = -math.inf
+
+    def _take(self, n):
+        v = self.g[self.cur:self.cur + n]
+        self.cur += n
+        return v
+
+    def select_action(self):
+        g = self._take(D)
+        return [_clip(f32(m + f32(0.0 + self.noise * x)), f32(-1), f32(1)) for m, x in zip(self.mean, g)]
+
+    def update(self, reward):
+        if reward > self.best:
+            g = self._take(D)
+            self.mean = [_clip(f32(float(m) + (0.0 + self.lr * x)), f32(-self.clip), f32(self.clip))
+                         for m, x in zip(self.mean, g)]
+            self.best = reward
+
+    def reset(self):
+        self.best = -math.inf
+
+
+def oracle_run_episode(env: OracleEnv, pol: OracleSimpleLearner, draws, max_steps=None):
+    """training/episode_utils.py:13-55 with the training-loop success rule
+    (info has no "success" key, :52) -> success is always False."""
+    env.reset(draws)
+    pol.reset()
+    max_steps = max_steps or env.max_episode_steps
+    total = 0.0
+    step = 0
+    for step in range(max_steps):
+        a = pol.select_action()
+        _, r, term, trunc = env.step(a)
+        total += r
+        pol.update(r)
+        if term or trunc:
+            break
+    return False, step + 1, total
+
+
+def oracle_noisy_action(action, noise):
+    """evaluation/robustness_tests.py:180-187: a' = clip(a + f32(n), low, high)."""
+    return [_clip(f32(f32(a) + f32(n)), f32(-1), f32(1)) for a, n in zip(action, noise)]
+
+
+def oracle_noisy_obs(obs, noise):
+    """evaluation/robustness_tests.py:199-207: obs + f32(n) (f32 add)."""
+    return (obs + np.asarray(noise).astype(np.float32)).astype(np.float32)

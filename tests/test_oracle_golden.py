@@ -1,0 +1,126 @@
+"""Pin the CPU oracle against fixtures captured from the reference itself."""
+import math
+
+import numpy as np
+import pytest
+
+import golden_io as G
+from oracle.dx_oracle import (OracleCurriculum, OracleEnv, OracleSimpleLearner, oracle_noisy_action,
+                              oracle_noisy_obs, oracle_run_episode, reset_draws)
+
+
+def _pcg(seed):
+    return np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+
+
+def _nan_equal(a, b):
+    return np.array_equal(np.asarray(a), np.asarray(b), equal_nan=True)
+
+
+ENV_CASES = G.meta()["env_cases"]
+
+
+@pytest.mark.parametrize("case", ENV_CASES, ids=lambda c: f"c{c['index']}-{c['cfg']}-{c['reward']}")
+def test_env_trace_bit_exact(case):
+    z = G.env_case(case["index"])
+    cur = OracleCurriculum.from_record(case["curriculum"])
+    env = OracleEnv(cur=cur, dense=case["reward"] == "dense", max_episode_steps=case["max_episode_steps"],
+                    object_position=case.get("object_position"))
+    rng = _pcg(case["seed"])
+    first = case.get("object_position") is None
+    for e in range(case["E"]):
+        d = reset_draws(rng, cur, first)
+        first = False
+        assert _nan_equal(d, z["draws"][e])  # host RNG mirror == reference draw order
+        obs = env.reset(d)
+        assert np.array_equal(obs, z["reset_obs"][e])
+        assert np.array_equal(np.array(env.op), z["reset_op"][e])
+        assert env.num_contacts == z["reset_ncon"][e]
+        assert [env.size, env.mass, env.fric] == list(z["reset_params"][e])
+        for t in range(z["length"][e]):
+            obs, r, term, trunc = env.step(z["actions"][e, t])
+            assert np.array_equal(obs, z["obs"][e, t]), (e, t)
+            assert math.isclose(r, z["reward"][e, t], rel_tol=1e-12, abs_tol=1e-15), (e, t)
+            np.testing.assert_allclose(env.last_components, z["comps"][e, t], rtol=1e-12, atol=1e-15)
+            assert term == bool(z["term"][e, t]) and trunc == bool(z["trunc"][e, t])
+            assert env.num_contacts == z["ncon"][e, t]
+            assert np.array_equal(np.array(env.op), z["op"][e, t])
+            assert env.t == z["step_count"][e, t]
+
+
+LEARNER_CASES = G.meta()["learner_cases"]
+
+
+@pytest.mark.parametrize("case", LEARNER_CASES, ids=lambda c: f"l{c['index']}-{c['cfg']}")
+def test_run_episode_simple_learner(case):
+    z = G.learner_case(case["index"])
+    cur = OracleCurriculum.from_record(case["curriculum"])
+    env = OracleEnv(cur=cur, dense=case["reward"] == "dense",
+                    max_episode_steps=case.get("max_episode_steps", 200))
+    gauss = np.random.RandomState(case["learner_seed"]).standard_normal(200_000)
+    pol = OracleSimpleLearner(gauss, learning_rate=case["lr"])
+    rng = _pcg(case["env_seed"])
+    k = 0
+    for e in range(case["episodes"]):
+        draws = reset_draws(rng, cur, first=(e == 0))
+        # step-level replay of run_episode to compare per-step learner state
+        env.reset(draws)
+        pol.reset()
+        total = 0.0
+        for step in range(case["max_steps"]):
+            a = pol.select_action()
+            assert np.array_equal(np.array(a, np.float32), z["action"][k]), (e, step)
+            _, r, term, trunc = env.step(a)
+            assert math.isclose(r, z["reward"][k], rel_tol=1e-12, abs_tol=1e-15)
+            total += r
+            pol.update(r)
+            assert np.array_equal(np.array(pol.mean, np.float32), z["mean"][k])
+            k += 1
+            if term or trunc:
+                break
+        assert step + 1 == z["ep_steps"][e]
+        assert math.isclose(total, z["ep_return"][e], rel_tol=1e-12)
+        assert z["ep_success"][e] == 0  # training-loop success is always False (quirk 3)
+    assert k == len(z["action"])
+
+
+def test_run_episode_function_matches():
+    case = LEARNER_CASES[0]
+    z = G.learner_case(0)
+    cur = OracleCurriculum.from_record(case["curriculum"])
+    env = OracleEnv(cur=cur, dense=True)
+    pol = OracleSimpleLearner(np.random.RandomState(case["learner_seed"]).standard_normal(100_000),
+                              learning_rate=case["lr"])
+    rng = _pcg(case["env_seed"])
+    for e in range(case["episodes"]):
+        s, n, tot = oracle_run_episode(env, pol, reset_draws(rng, cur, e == 0), case["max_steps"])
+        assert (s, n) == (False, z["ep_steps"][e])
+        assert math.isclose(tot, z["ep_return"][e], rel_tol=1e-12)
+
+
+NOISE_CASES = G.meta()["noise_cases"]
+
+
+@pytest.mark.parametrize("ci", range(len(NOISE_CASES)))
+def test_noise_wrapper(ci):
+    c = NOISE_CASES[ci]
+    z = G.noise_case(ci)
+    rec = G.meta()["host"]["configs"][c["cfg"]]
+    cur = OracleCurriculum.from_record(rec)
+    env = OracleEnv(cur=cur, dense=True)
+    nrng = np.random.default_rng(c["seed"])  # one wrapper rng (robustness_tests.py:164)
+    for e in range(c["episodes"]):
+        rng = _pcg(c["seed"] + e)  # env.reset(seed=seed+episode)
+        obs = env.reset(reset_draws(rng, cur, first=(e == 0)))
+        if c["obs_std"] > 0:
+            obs = oracle_noisy_obs(obs, nrng.normal(0, c["obs_std"], size=45))
+        assert np.array_equal(obs, z["reset_obs"][e])
+        for t in range(z["length"][e]):
+            a = z["actions"][e, t]
+            if c["dyn_std"] > 0:
+                a = oracle_noisy_action(a, nrng.normal(0, c["dyn_std"], size=15))
+            obs, r, term, trunc = env.step(a)
+            if c["obs_std"] > 0:
+                obs = oracle_noisy_obs(obs, nrng.normal(0, c["obs_std"], size=45))
+            assert np.array_equal(obs, z["obs"][e, t]), (e, t)
+            assert math.isclose(r, z["reward"][e, t], rel_tol=1e-12, abs_tol=1e-15)

@@ -1,0 +1,216 @@
+"""Benchmark: env-steps/sec of the vectorised rollout hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--horizon 200]
+
+One bench "step" = one training iteration of the hot path over one batch:
+every env of the shard advances `horizon` env steps (select_action -> step ->
+reward -> learner update, auto-reset at episode end) -- the reference's
+run_episode + SimpleLearner loop (training/episode_utils.py:13-55) fused into
+one HIP launch.  Workload = BASELINE configs[1]: config_easy curriculum,
+dense reward, 4096 envs per GPU, synthetic (device Philox) randomness.
+
+Multi-GPU (torchrun, one rank per GPU): env shards are independent replicas
+(global env ids rank*N .. rank*N+N-1), no data-path collective; the timing
+uses a barrier + max-over-ranks.  value = all ranks' env steps / max time.
+
+Also measured in-process (HIP events on the launch stream):
+  * roofline: the standalone step kernel (dxrl_env_step, k_step) at a large N
+    (default 2^22 envs, traffic >> the 256 MB Infinity Cache) -- the
+    "%HBM roofline step kernel" half of the BASELINE metric;
+  * cpu_baseline: the CPU oracle's run_episode + SimpleLearner loop (the
+    reference's algorithm restated), one core, a bounded ~10 s sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+STEP_BYTES_PER_ENV = 594  # k_step algorithmic bytes per env-step
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    p.add_argument("--horizon", type=int, default=200, help="env steps per bench step (rollout length)")
+    p.add_argument("--curriculum", default="easy")
+    p.add_argument("--roofline-envs", type=int, default=1 << 22)
+    p.add_argument("--roofline-launches", type=int, default=30)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-roofline", action="store_true")
+    return p.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def rollout_bench(args, world, rank, dev):
+    import dexterous_rl_manipulation_amd as pkg
+    from dexterous_rl_manipulation_amd import envs, policies, training
+    n = args.envs
+    env = envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.named(args.curriculum), reward_type="dense",
+                      seed=20240601, device=dev, global_env_offset=rank * n)
+    learner = policies.VecSimpleLearner(n, seed=777, device=dev)
+    ro = training.SimpleLearnerRollout(env, learner)
+    ro.start()
+    for _ in range(args.warmup):
+        ro.run(args.horizon, collect=False)
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        ro.run(args.horizon, collect=False)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    wall = max_over_ranks(wall, world, dev)
+    # bookkeeping check outside the timed region
+    rec = ro.run(args.horizon)
+    assert rec.dropped == 0 and len(rec) > 0
+    return wall, kernel_ms
+
+
+def step_kernel_roofline(args, dev):
+    """k_step at large N: algorithmic bytes / HIP-event time per launch."""
+    from dexterous_rl_manipulation_amd import envs
+    import dexterous_rl_manipulation_amd as pkg
+    n = args.roofline_envs
+    env = envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.variable(), reward_type="dense", seed=5,
+                      device=dev)
+    env.reset(write_obs=False)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0)
+    acts = (torch.rand(n, 15, generator=gen, device=dev) * 2.4 - 1.2).contiguous()
+    for _ in range(3):
+        env.step(acts)
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.roofline_launches + 1)]
+    evs[0].record(stream)
+    for k in range(args.roofline_launches):
+        env.step(acts)
+        evs[k + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    per = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.roofline_launches)]
+    ms = float(np.mean(per))
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            d = json.load(f)
+        if d.get("envs") == n:
+            traffic = d.get("hbm_bytes_per_launch")
+    bytes_per_launch = STEP_BYTES_PER_ENV * n
+    achieved = bytes_per_launch / (ms * 1e-3) / 1e9
+    del env, acts
+    torch.cuda.empty_cache()
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "kernel": "k_step (dxrl_env_step)",
+            "envs": n, "bytes_per_env_step": STEP_BYTES_PER_ENV, "ms_per_launch": round(ms, 4),
+            "env_steps_per_s": round(n / (ms * 1e-3), 1)}
+
+
+def cpu_baseline(args):
+    """The reference algorithm restated (oracle/dx_oracle.py) in the reference's
+    own loop shape: run_episode + SimpleLearner, one env, one core."""
+    from oracle.dx_oracle import OracleCurriculum, OracleEnv, OracleSimpleLearner, reset_draws
+    presets = {"easy": dict(object_size=0.08, object_mass=0.05, friction_coefficient=0.8),
+               "medium": {}, "hard": dict(object_size=0.03, object_mass=0.2, friction_coefficient=0.3)}
+    cur = OracleCurriculum(**presets.get(args.curriculum, {}))
+    env = OracleEnv(cur=cur, dense=True)
+    pol = OracleSimpleLearner(np.random.RandomState(42).standard_normal(4_000_000), learning_rate=0.01)
+    rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence(1000)))
+    steps = 0
+    first = True
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds and pol.cur < 3_900_000:
+        env.reset(reset_draws(rng, cur, first))
+        first = False
+        pol.reset()
+        for _ in range(200):
+            a = pol.select_action()
+            _, r, te, tr = env.step(a)
+            pol.update(r)
+            steps += 1
+            if te or tr:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": round(steps / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/dx_oracle.py run_episode+SimpleLearner loop, config_{args.curriculum}, 1 env, "
+                      f"{steps} env-steps in {dt:.1f} s on 1 host core"}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    dev = torch.device("cuda", local if world > 1 else 0)
+    wall, kernel_ms = rollout_bench(args, world, rank, dev)
+    total_steps = args.envs * world * args.horizon * args.steps
+    value = total_steps / wall
+    out = {
+        "metric": "env-steps/sec @4096 envs/GPU, 1/2/4/8 MI355X; %HBM roofline step kernel",
+        "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32+f64",
+        "data": "synthetic (device Philox4x32-10 reset draws and learner noise)",
+        "config": {"workload": f"config_{args.curriculum}.json fused rollout: run_episode x SimpleLearner, dense "
+                               f"reward, {args.horizon} env steps per bench step",
+                   "envs_per_gpu": args.envs, "global_envs": args.envs * world, "horizon": args.horizon,
+                   "parallelism": f"env-shard replicas x{world} (no collective)",
+                   "rollout_kernel_ms": round(kernel_ms, 4)},
+    }
+    if rank == 0 and not args.no_roofline:
+        out["roofline"] = step_kernel_roofline(args, dev)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,159 @@
+"""ctypes binding of libdxrl.so (the C ABI declared in include/dxrl.h).
+
+The library is built in-tree by ``build.build_native()`` (hipcc, gfx950) and
+loaded here.  There is no fallback: if the library is missing or no GPU is
+visible, every product entry point raises.  torch is imported first so the
+library binds to the HIP runtime torch already loaded (one runtime per
+process; streams and device pointers are shared).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch  # noqa: F401  (loads libamdhip64 first; see module docstring)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libdxrl.so")
+
+DXRL_OK = 0
+DXRL_E_INVALID = -1
+DXRL_E_HIP = -2
+DXRL_E_UNSUPPORTED = -3
+DXRL_E_TAPE = -4
+REWARD_SPARSE = 0
+REWARD_DENSE = 1
+RESET_EXTRA = 6
+MAX_CURRICULA = 256
+SUCCESS_TRAINING = 0
+SUCCESS_TERMINATED = 1
+ABI_VERSION = 1
+
+
+class Curriculum(C.Structure):
+    _fields_ = [("object_size", C.c_double), ("object_mass", C.c_double), ("friction_coefficient", C.c_double),
+                ("size_range", C.c_double * 2), ("mass_range", C.c_double * 2), ("friction_range", C.c_double * 2),
+                ("spawn_x_range", C.c_double * 2), ("spawn_y_range", C.c_double * 2),
+                ("spawn_z_range", C.c_double * 2),
+                ("has_size_range", C.c_int32), ("has_mass_range", C.c_int32), ("has_friction_range", C.c_int32),
+                ("friction_is_f64_scalar", C.c_int32)]
+
+
+class EnvConfig(C.Structure):
+    _fields_ = [("num_envs", C.c_int32), ("num_fingers", C.c_int32), ("joints_per_finger", C.c_int32),
+                ("max_episode_steps", C.c_int32), ("reward_type", C.c_int32), ("has_object_position", C.c_int32),
+                ("object_position", C.c_double * 3),
+                ("distance_weight", C.c_double), ("contact_weight", C.c_double), ("closure_weight", C.c_double),
+                ("stability_weight", C.c_double), ("seed", C.c_uint64), ("global_env_offset", C.c_int64)]
+
+
+class EnvLayout(C.Structure):
+    _fields_ = [(k, C.c_int64) for k in ("total_bytes", "jp", "jv", "op", "ov", "flags", "step_count", "size",
+                                         "mass", "friction", "cfg_index", "reset_ctr", "curricula")]
+
+
+class LearnerLayout(C.Structure):
+    _fields_ = [(k, C.c_int64) for k in ("total_bytes", "mean", "best", "ep_return", "noise_ctr")]
+
+
+class LearnerConfig(C.Structure):
+    _fields_ = [("learning_rate", C.c_double), ("exploration_noise", C.c_double),
+                ("action_clip_range", C.c_double), ("seed", C.c_uint64)]
+
+
+class RolloutIO(C.Structure):
+    _fields_ = [("gauss", C.c_void_p), ("gauss_stride", C.c_int64), ("reset_draws", C.c_void_p),
+                ("reset_stride", C.c_int64), ("record_cap", C.c_int32), ("ep_return", C.c_void_p),
+                ("ep_length", C.c_void_p), ("ep_success", C.c_void_p), ("ep_end_step", C.c_void_p),
+                ("ep_count", C.c_void_p), ("gauss_used", C.c_void_p), ("status", C.c_void_p)]
+
+
+_P = C.c_void_p
+_SIGS = {
+    "dxrl_abi_version": (C.c_int, []),
+    "dxrl_last_error": (C.c_char_p, []),
+    "dxrl_env_layout_for": (C.c_int, [C.POINTER(EnvConfig), C.POINTER(EnvLayout)]),
+    "dxrl_env_create": (C.c_int, [C.POINTER(EnvConfig), C.c_int32, _P, _P, C.POINTER(_P)]),
+    "dxrl_env_destroy": (C.c_int, [_P]),
+    "dxrl_env_set_curricula": (C.c_int, [_P, C.POINTER(Curriculum), C.c_int32, _P, _P]),
+    "dxrl_env_reset": (C.c_int, [_P, _P, _P, _P, _P]),
+    "dxrl_env_step": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    "dxrl_env_observe": (C.c_int, [_P, _P, _P]),
+    "dxrl_env_set_max_episode_steps": (C.c_int, [_P, C.c_int32]),
+    "dxrl_learner_layout_for": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(LearnerLayout)]),
+    "dxrl_learner_init": (C.c_int, [C.c_int32, C.c_int32, _P, _P]),
+    "dxrl_learner_reset": (C.c_int, [C.c_int32, C.c_int32, _P, _P, _P]),
+    "dxrl_learner_select": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_double, _P, _P, _P]),
+    "dxrl_learner_update": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_double, C.c_double, _P, _P, _P, _P]),
+    "dxrl_rollout_simple": (C.c_int, [_P, _P, C.POINTER(LearnerConfig), C.c_int32, C.c_int32, C.c_int32,
+                                      C.POINTER(RolloutIO), _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libdxrl.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                                  "(there is no CPU fallback)")
+            h = C.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(h, name)
+                fn.restype = res
+                fn.argtypes = args
+            if h.dxrl_abi_version() != ABI_VERSION:
+                raise NativeError("libdxrl.so ABI version mismatch; rebuild")
+            _lib = h
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc == DXRL_OK:
+        return
+    msg = lib().dxrl_last_error().decode(errors="replace")
+    if rc in (DXRL_E_INVALID, DXRL_E_UNSUPPORTED):
+        raise ValueError(f"{what}: {msg}")
+    raise NativeError(f"{what}: {msg} (status {rc})")
+
+
+def call(name: str, *args):
+    check(getattr(lib(), name)(*args), name)
+
+
+def ptr(t) -> int | None:
+    """Device address of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu(device=None) -> torch.device:
+    if not torch.cuda.is_available():
+        raise NativeError("no HIP device visible: the dxrl hot path runs only on the GPU (no CPU fallback)")
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if dev.type != "cuda":
+        raise ValueError(f"device must be a GPU device, got {dev}")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
+def aligned_empty(nbytes: int, device, align: int = 256):
+    """uint8 device buffer whose data_ptr is `align`-aligned; returns (owner, view)."""
+    owner = torch.empty(nbytes + align, dtype=torch.uint8, device=device)
+    off = (-owner.data_ptr()) % align
+    return owner, owner[off:off + nbytes]

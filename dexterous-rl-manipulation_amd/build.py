@@ -1,0 +1,50 @@
+"""In-tree build of libdxrl.so for gfx950 (hipcc; no cmake, no JIT cache).
+
+The built library lives next to this file so it travels with the repository
+snapshot to the GPU box.  Numerics flags are part of the contract:
+``-ffp-contract=off`` (the reference never fuses a multiply-add) and
+correctly rounded f32 division/sqrt.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+SOURCES = ["dxrl_env.hip", "dxrl_rollout.hip"]
+HEADERS = ["dxrl_device.h", "dxrl_internal.h"]
+OUT = os.path.join(PKG_DIR, "libdxrl.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-ffp-contract=off",
+         "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function"]
+
+
+def _inputs():
+    root = os.path.dirname(PKG_DIR)
+    files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    files.append(os.path.join(root, "include", "dxrl.h"))
+    return files
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(f) <= t for f in _inputs())
+
+
+def build_native(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return OUT
+    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build_native(force=True, verbose=True))

@@ -1,0 +1,340 @@
+// dxrl_device.h -- per-env physics, contacts and reward terms for gfx950.
+//
+// One lane owns one env; every per-env quantity lives in registers.  The
+// arithmetic restates the reference op by op under NumPy-2 (NEP 50) scalar
+// promotion -- f32 where the reference's arrays are f32, f64 where NumPy
+// promotes -- and the library is compiled with -ffp-contract=off so no
+// multiply-add is fused (the reference never fuses).  Citations are into the
+// reference checkout (envs/manipulation_env.py = ME, rewards/reward_shaping.py = RS,
+// policies/simple_learner.py = SL).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dxrl.h"
+
+namespace dxrl {
+
+constexpr int kF = 5, kJ = 3, kD = kF * kJ;  // ME:26-27 defaults (compiled shape)
+constexpr int kObs = 2 * kD + 10 + kF;       // ME:96-100 -> 45
+constexpr int kReset = kD + DXRL_RESET_EXTRA;
+
+// Python-float literals as NumPy sees them next to an f32 array: the double
+// rounded to f32 (NEP 50 weak scalar), not the decimal rounded to f32.
+constexpr float kC09 = (float)0.9, kC01 = (float)0.1, kDt = (float)0.01;
+constexpr double kGz = -9.81 * 0.01;  // ME:211-212 gravity (f64)
+constexpr double kLo[3] = {-0.2, -0.2, 0.0}, kHi[3] = {0.2, 0.2, 0.3};  // ME:119
+
+// flag word bits
+constexpr uint32_t kPrevShift = 8, kHasPrev = 1u << 16, kOpIsF32 = 1u << 17, kHasObject = 1u << 18,
+                   kFricF64 = 1u << 19;  // episode friction is a numpy.float64 (NEP 50 f64 damping)
+
+struct Weights {
+    double w_dist, w_con, w_clo, w_st;
+};
+
+// np.clip / np.minimum(np.maximum(x, lo), hi) without NaN canonicalisation.
+__device__ __forceinline__ float clipf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+__device__ __forceinline__ double clipd(double x, double lo, double hi) {
+    double y = x < lo ? lo : x;  // np.maximum(x, lo)
+    return y > hi ? hi : y;      // np.minimum(., hi)
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct u32x4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+// 53-bit uniform in [0,1), as numpy's next_double((u64 >> 11) * 2^-53)
+__device__ __forceinline__ double u01_53(uint32_t hi, uint32_t lo) {
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    return (double)(v >> 11) * (1.0 / 9007199254740992.0);
+}
+// 24-bit uniform in (0,1]
+__device__ __forceinline__ float u01_24(uint32_t v) { return ((float)(v >> 8) + 1.0f) * (1.0f / 16777216.0f); }
+// two standard normals (Box-Muller, f32) from two u32
+__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& n0, float& n1) {
+    const float r = sqrtf(-2.0f * __logf(u01_24(a)));
+    float s, c;
+    __sincosf(6.28318530717958647692f * u01_24(b), &s, &c);
+    n0 = r * c;
+    n1 = r * s;
+}
+
+// Stream ids for the Philox counter's third word.
+constexpr uint32_t kStreamReset = 0x52535400u, kStreamPolicy = 0x504f4c00u, kStreamDyn = 0x44594e00u,
+                   kStreamObs = 0x4f425300u;
+
+__device__ __forceinline__ void env_key(uint64_t seed, int64_t gid, uint32_t& k0, uint32_t& k1) {
+    k0 = (uint32_t)gid ^ (uint32_t)(seed >> 32) * 0x85EBCA6Bu;
+    k1 = (uint32_t)seed ^ (uint32_t)((uint64_t)gid >> 32) * 0xC2B2AE35u;
+}
+
+// ---------------------------------------------------------------- env registers
+struct Env {
+    float jp[kD], jv[kD];
+    double op[3];
+    float ov[3];
+    uint32_t flags;
+    int32_t t;
+    double size, mass, fric;
+    int32_t cfg;
+};
+
+// ME:285-310 _update_contacts.  tip_f = f64(f32(f32(sum_seq joints) * 0.1f)),
+// d_f = sqrt(((tx-ox)^2 + (ty-oy)^2) + (tz-oz)^2) in f64 (np.linalg.norm axis=1),
+// contact_f = d_f < size * 1.5.  Returns the contact bitmask; min distance out.
+__device__ __forceinline__ uint32_t contacts_of(const Env& e, double& dmin) {
+    const double thr = e.size * 1.5;
+    uint32_t mask = 0;
+    dmin = 0.0;
+#pragma unroll
+    for (int f = 0; f < kF; ++f) {
+        float s = e.jp[kJ * f];
+#pragma unroll
+        for (int j = 1; j < kJ; ++j) s = s + e.jp[kJ * f + j];
+        const double tip = (double)(s * kC01);
+        const double dx = tip - e.op[0], dy = tip - e.op[1], dz = tip - e.op[2];
+        const double d = sqrt((dx * dx + dy * dy) + dz * dz);
+        mask |= (d < thr ? 1u : 0u) << f;
+        dmin = (f == 0 || d < dmin) ? d : dmin;  // np.min
+    }
+    return mask;
+}
+
+// RS:101-187 dense terms + weighted total (RS:84-89); updates prev contacts.
+__device__ __forceinline__ double dense_reward(Env& e, uint32_t c, double dmin, const Weights& w, double comp[4]) {
+    const double dist = exp(-5.0 * dmin);                 // RS:111-116
+    const int n = __popc(c);
+    const double con = (double)n / (double)kF;            // RS:128-134
+    float sum = 0.0f;                                     // RS:147-162
+#pragma unroll
+    for (int f = 0; f < kF; ++f) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) {
+            const float v = e.jp[kJ * f + j];
+            if (v < 0.0f) acc = acc + v;
+        }
+        sum = sum + (-acc);
+    }
+    const float avg = sum / (float)kF;
+    const float clo = clipf(avg / (float)kF, 0.0f, 1.0f);
+    float st = 0.0f;                                      // RS:166-187
+    if (e.flags & kHasPrev) {
+        const uint32_t prev = (e.flags >> kPrevShift) & 0xFFu;
+        float ch = 0.0f;
+#pragma unroll
+        for (int f = 0; f < kF; ++f) ch = ch + (float)(((c ^ prev) >> f) & 1u);
+        st = clipf(1.0f - ch / (float)kF, 0.0f, 1.0f);
+    }
+    e.flags = (e.flags & ~(0xFFu << kPrevShift)) | (c << kPrevShift) | kHasPrev;
+    comp[0] = dist;
+    comp[1] = con;
+    comp[2] = (double)clo;
+    comp[3] = (double)st;
+    return ((w.w_dist * dist + w.w_con * con) + w.w_clo * (double)clo) + w.w_st * (double)st;
+}
+
+// ME:198-252 one step.  a[] = raw action (clipped here, ME:199).
+// Returns reward; term/trunc flags; comp[] the reward components.
+__device__ __forceinline__ double env_step(Env& e, const float* a, bool dense, const Weights& w,
+                                           int max_episode_steps, bool& term, bool& trunc, double comp[4]) {
+#pragma unroll
+    for (int k = 0; k < kD; ++k) {
+        const float ak = clipf(a[k], -1.0f, 1.0f);
+        e.jv[k] = kC09 * e.jv[k] + kC01 * ak;                  // ME:203 (f32, no FMA)
+        e.jp[k] = clipf(e.jp[k] + e.jv[k] * kDt, -1.0f, 1.0f);  // ME:204-207
+    }
+    const double damp = 1.0 - (e.fric * 0.1 * 0.01);  // ME:215
+    const float dampf = (float)damp;
+    const double g[3] = {0.0, 0.0, kGz};
+    const bool op32 = (e.flags & kOpIsF32) != 0;
+    const bool fric_f64 = (e.flags & kFricF64) != 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        float v = fric_f64 ? (float)((double)e.ov[i] * damp) : e.ov[i] * dampf;  // ME:216 (NEP 50)
+        v = (float)((double)v + g[i]);                                          // ME:219 f32 += f64
+        const float inc = v * kDt;                                              // ME:222
+        double p = op32 ? (double)((float)e.op[i] + inc) : e.op[i] + (double)inc;
+        p = clipd(p, kLo[i], kHi[i]);                                           // ME:225-229 -> f64
+        if ((p <= kLo[i] && v < 0.0f) || (p >= kHi[i] && v > 0.0f)) v = 0.0f;   // ME:232-235
+        e.op[i] = p;
+        e.ov[i] = v;
+    }
+    e.flags &= ~kOpIsF32;
+    double dmin;
+    const uint32_t c = contacts_of(e, dmin);                                    // ME:238
+    double r;
+    if (dense) {
+        r = dense_reward(e, c, dmin, w, comp);
+    } else {
+        r = (__popc(c) >= 3) ? 1.0 : -0.01;  // RS:226-231
+        comp[0] = comp[1] = comp[2] = comp[3] = 0.0;
+    }
+    e.flags = (e.flags & ~0xFFu) | c;
+    term = __popc(c) >= 3;                   // ME:332-336
+    trunc = e.t >= max_episode_steps;        // ME:245 (before the increment)
+    e.t += 1;                                // ME:247
+    return r;
+}
+
+// ME:124-182 reset from resolved draws (see DXRL_RESET_EXTRA slot order).
+__device__ __forceinline__ void env_reset(Env& e, const double* draw, const dxrl_curriculum& cu) {
+#pragma unroll
+    for (int k = 0; k < kD; ++k) {
+        e.jp[k] = (float)draw[k];  // ME:143-145 .astype(float32)
+        e.jv[k] = 0.0f;
+    }
+    e.size = cu.has_size_range ? draw[kD + 0] : cu.object_size;  // config.py:44-84
+    e.mass = cu.has_mass_range ? draw[kD + 1] : cu.object_mass;
+    e.fric = cu.has_friction_range ? draw[kD + 2] : cu.friction_coefficient;
+    const bool has = (e.flags & kHasObject) != 0;  // ME:156-161 sticky position
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        e.op[i] = (double)(float)(has ? e.op[i] : draw[kD + 3 + i]);
+        e.ov[i] = 0.0f;
+    }
+    e.t = 0;
+    // prev_contacts = None (RS:45-48); the host marks rows whose episode friction is a numpy.float64
+    e.flags = kOpIsF32 | kHasObject | (cu.friction_is_f64_scalar ? kFricF64 : 0u);
+    double dmin;
+    e.flags |= contacts_of(e, dmin);  // ME:176
+}
+
+// Device-RNG reset draws: the same slots, uniform(lo, hi) = lo + (hi-lo)*u.
+__device__ __forceinline__ void philox_reset_draws(double* d, const dxrl_curriculum& cu, uint32_t k0, uint32_t k1,
+                                                   uint64_t ctr) {
+    uint32_t u[2 * kReset + 2];
+#pragma unroll
+    for (int b = 0; b < (2 * kReset + 3) / 4; ++b) {
+        const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamReset, (uint32_t)b}, k0, k1);
+        if (4 * b + 0 < 2 * kReset + 2) u[4 * b + 0] = r.x;
+        if (4 * b + 1 < 2 * kReset + 2) u[4 * b + 1] = r.y;
+        if (4 * b + 2 < 2 * kReset + 2) u[4 * b + 2] = r.z;
+        if (4 * b + 3 < 2 * kReset + 2) u[4 * b + 3] = r.w;
+    }
+#pragma unroll
+    for (int k = 0; k < kD; ++k) d[k] = -0.1 + (0.1 - -0.1) * u01_53(u[2 * k], u[2 * k + 1]);
+    const double* rng[6] = {cu.size_range, cu.mass_range, cu.friction_range,
+                            cu.spawn_x_range, cu.spawn_y_range, cu.spawn_z_range};
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        d[kD + k] = rng[k][0] + (rng[k][1] - rng[k][0]) * u01_53(u[2 * (kD + k)], u[2 * (kD + k) + 1]);
+}
+
+__device__ __forceinline__ void write_obs(const Env& e, float* o) {  // ME:254-264
+#pragma unroll
+    for (int k = 0; k < kD; ++k) o[k] = e.jp[k];
+#pragma unroll
+    for (int k = 0; k < kD; ++k) o[kD + k] = e.jv[k];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o[2 * kD + i] = (float)e.op[i];
+    o[2 * kD + 3] = 1.0f;  // identity quaternion (ME:164)
+    o[2 * kD + 4] = 0.0f;
+    o[2 * kD + 5] = 0.0f;
+    o[2 * kD + 6] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o[2 * kD + 7 + i] = e.ov[i];
+#pragma unroll
+    for (int f = 0; f < kF; ++f) o[2 * kD + 10 + f] = (float)((e.flags >> f) & 1u);
+}
+
+// ---------------------------------------------------------------- SoA access
+struct EnvSoA {
+    float* jp;
+    float* jv;
+    double* op;
+    float* ov;
+    uint32_t* flags;
+    int32_t* t;
+    double *size, *mass, *fric;
+    int32_t* cfg;
+    uint64_t* reset_ctr;
+    double* comps;
+    const dxrl_curriculum* curricula;
+    int64_t n;
+};
+
+__device__ __forceinline__ void load_env(const EnvSoA& s, int64_t i, Env& e) {
+#pragma unroll
+    for (int k = 0; k < kD; ++k) {
+        e.jp[k] = s.jp[k * s.n + i];
+        e.jv[k] = s.jv[k * s.n + i];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        e.op[k] = s.op[k * s.n + i];
+        e.ov[k] = s.ov[k * s.n + i];
+    }
+    e.flags = s.flags[i];
+    e.t = s.t[i];
+    e.size = s.size[i];
+    e.mass = s.mass[i];
+    e.fric = s.fric[i];
+    e.cfg = s.cfg[i];
+}
+
+// Step-only traffic: the episode constants (size, friction) are read, never
+// written; mass and the curriculum row are not touched by a step.
+__device__ __forceinline__ void load_env_dyn(const EnvSoA& s, int64_t i, Env& e) {
+#pragma unroll
+    for (int k = 0; k < kD; ++k) {
+        e.jp[k] = s.jp[k * s.n + i];
+        e.jv[k] = s.jv[k * s.n + i];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        e.op[k] = s.op[k * s.n + i];
+        e.ov[k] = s.ov[k * s.n + i];
+    }
+    e.flags = s.flags[i];
+    e.t = s.t[i];
+    e.size = s.size[i];
+    e.fric = s.fric[i];
+}
+
+__device__ __forceinline__ void store_env_dyn(const EnvSoA& s, int64_t i, const Env& e) {
+#pragma unroll
+    for (int k = 0; k < kD; ++k) {
+        s.jp[k * s.n + i] = e.jp[k];
+        s.jv[k * s.n + i] = e.jv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        s.op[k * s.n + i] = e.op[k];
+        s.ov[k * s.n + i] = e.ov[k];
+    }
+    s.flags[i] = e.flags;
+    s.t[i] = e.t;
+}
+
+__device__ __forceinline__ void store_env(const EnvSoA& s, int64_t i, const Env& e) {
+#pragma unroll
+    for (int k = 0; k < kD; ++k) {
+        s.jp[k * s.n + i] = e.jp[k];
+        s.jv[k * s.n + i] = e.jv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        s.op[k * s.n + i] = e.op[k];
+        s.ov[k * s.n + i] = e.ov[k];
+    }
+    s.flags[i] = e.flags;
+    s.t[i] = e.t;
+    s.size[i] = e.size;
+    s.mass[i] = e.mass;
+    s.fric[i] = e.fric;
+}
+
+}  // namespace dxrl

@@ -1,0 +1,329 @@
+// dxrl_env.hip -- batched env reset/step kernels and the env half of the C ABI.
+//
+// Replaces envs/manipulation_env.py (DexterousManipulationEnv) + the reward
+// plugins of rewards/reward_shaping.py.  State is a struct-of-arrays slab in
+// HBM (layout in include/dxrl.h): component-major, env-contiguous, so every
+// per-component access of a wave is one coalesced 256-B (f32) / 512-B (f64)
+// transaction.  Row-major I/O tensors (actions [N][15], obs [N][45]) are
+// staged through LDS so their HBM traffic is coalesced too.
+#include <cmath>
+#include <cstring>
+#include <new>
+
+#include "dxrl_internal.h"
+
+using namespace dxrl;
+
+namespace dxrl {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+// ----------------------------------------------------------------------- init
+__global__ void k_init(EnvSoA s, int has_obj, double ox, double oy, double oz) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= s.n) return;
+    Env e;
+#pragma unroll
+    for (int k = 0; k < kD; ++k) e.jp[k] = e.jv[k] = 0.0f;
+    e.op[0] = ox;
+    e.op[1] = oy;
+    e.op[2] = oz;
+    e.ov[0] = e.ov[1] = e.ov[2] = 0.0f;
+    e.flags = has_obj ? kHasObject : 0u;
+    e.t = 0;
+    e.size = e.mass = e.fric = 0.0;
+    store_env(s, i, e);
+    s.cfg[i] = 0;
+    s.reset_ctr[i] = 0;
+}
+
+// ----------------------------------------------------------------------- reset
+// ME:124-182.  One lane per env; reset is per-episode, not per-step, so the
+// obs row is written directly.
+__global__ __launch_bounds__(kBlock) void k_reset(EnvSoA s, const uint8_t* __restrict__ mask,
+                                                  const double* __restrict__ draws, float* __restrict__ obs,
+                                                  uint64_t seed, int64_t gid0) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= s.n) return;
+    if (mask && !mask[i]) return;
+    Env e;
+    load_env(s, i, e);
+    const dxrl_curriculum cu = s.curricula[e.cfg];
+    double d[kReset];
+    if (draws) {
+#pragma unroll
+        for (int k = 0; k < kReset; ++k) d[k] = draws[i * kReset + k];
+    } else {
+        uint32_t k0, k1;
+        env_key(seed, gid0 + i, k0, k1);
+        const uint64_t ctr = s.reset_ctr[i];
+        philox_reset_draws(d, cu, k0, k1, ctr);
+    }
+    s.reset_ctr[i] += 1;
+    env_reset(e, d, cu);
+    store_env(s, i, e);
+    if (obs) write_obs(e, obs + i * kObs);
+}
+
+// ----------------------------------------------------------------------- step
+// ME:184-252 fused with the reward plugin.  Block = 256 envs; actions and
+// observations move HBM<->LDS as contiguous float4 streams.
+template <bool kDense>
+__global__ __launch_bounds__(kBlock) void k_step(EnvSoA s, const float* __restrict__ act, float* __restrict__ obs,
+                                                 double* __restrict__ rew, uint8_t* __restrict__ term,
+                                                 uint8_t* __restrict__ trunc, double* __restrict__ comps, Weights w,
+                                                 int max_episode_steps) {
+    __shared__ __attribute__((aligned(16))) float lds[kBlock * kObs];
+    const int tid = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * kBlock;
+    const int nb = (int)min((int64_t)kBlock, s.n - base);
+
+    // actions [nb][15] -> LDS (coalesced float4; tail scalar)
+    {
+        const float* src = act + base * kD;
+        const int nf = nb * kD;
+        const int n4 = nf >> 2;
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        float4* l4 = reinterpret_cast<float4*>(lds);
+        for (int k = tid; k < n4; k += kBlock) l4[k] = s4[k];
+        for (int k = (n4 << 2) + tid; k < nf; k += kBlock) lds[k] = src[k];
+    }
+    __syncthreads();
+    Env e;
+    bool te = false, tr = false;
+    double r = 0.0, cp[4];
+    const int64_t i = base + tid;
+    if (tid < nb) {
+        load_env_dyn(s, i, e);
+        float a[kD];
+#pragma unroll
+        for (int k = 0; k < kD; ++k) a[k] = lds[tid * kD + k];
+        r = env_step(e, a, kDense, w, max_episode_steps, te, tr, cp);
+        store_env_dyn(s, i, e);
+        rew[i] = r;
+        term[i] = te;
+        trunc[i] = tr;
+        if (comps) {
+            double2* c2 = reinterpret_cast<double2*>(comps + i * 4);
+            c2[0] = double2{cp[0], cp[1]};
+            c2[1] = double2{cp[2], cp[3]};
+        }
+    }
+    if (!obs) return;
+    __syncthreads();
+    if (tid < nb) write_obs(e, lds + tid * kObs);
+    __syncthreads();
+    {
+        float* dst = obs + base * kObs;
+        const int nf = nb * kObs;
+        const int n4 = nf >> 2;
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        const float4* l4 = reinterpret_cast<const float4*>(lds);
+        for (int k = tid; k < n4; k += kBlock) d4[k] = l4[k];
+        for (int k = (n4 << 2) + tid; k < nf; k += kBlock) dst[k] = lds[k];
+    }
+}
+
+__global__ void k_observe(EnvSoA s, float* __restrict__ obs) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= s.n) return;
+    Env e;
+    load_env(s, i, e);
+    write_obs(e, obs + i * kObs);
+}
+
+static int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+int layout_for(const dxrl_env_config* cfg, dxrl_env_layout* L) {
+    const int64_t n = cfg->num_envs;
+    int64_t off = 0;
+    auto take = [&](int64_t bytes) {
+        const int64_t o = off;
+        off = align256(off + bytes);
+        return o;
+    };
+    L->jp = take(4 * kD * n);
+    L->jv = take(4 * kD * n);
+    L->op = take(8 * 3 * n);
+    L->ov = take(4 * 3 * n);
+    L->flags = take(4 * n);
+    L->step_count = take(4 * n);
+    L->size = take(8 * n);
+    L->mass = take(8 * n);
+    L->friction = take(8 * n);
+    L->cfg_index = take(4 * n);
+    L->reset_ctr = take(8 * n);
+    L->curricula = take((int64_t)sizeof(dxrl_curriculum) * DXRL_MAX_CURRICULA);
+    L->total_bytes = off;
+    return DXRL_OK;
+}
+
+static int validate_cfg(const dxrl_env_config* c) {
+    DXRL_REQUIRE(c != nullptr, "null config");
+    DXRL_REQUIRE(c->num_envs > 0, "num_envs must be > 0 (got %d)", c->num_envs);
+    if (c->num_fingers != kF || c->joints_per_finger != kJ) {
+        set_error("this build compiles num_fingers=%d, joints_per_finger=%d (got %d, %d)", kF, kJ, c->num_fingers,
+                  c->joints_per_finger);
+        return DXRL_E_UNSUPPORTED;
+    }
+    DXRL_REQUIRE(c->reward_type == DXRL_REWARD_DENSE || c->reward_type == DXRL_REWARD_SPARSE,
+                 "reward_type must be DXRL_REWARD_DENSE or DXRL_REWARD_SPARSE");
+    return DXRL_OK;
+}
+
+}  // namespace dxrl
+
+// =========================================================================== C ABI
+extern "C" {
+
+int dxrl_abi_version(void) { return DXRL_ABI_VERSION; }
+const char* dxrl_last_error(void) { return dxrl::g_err.c_str(); }
+
+int dxrl_env_layout_for(const dxrl_env_config* cfg, dxrl_env_layout* out) {
+    if (int rc = validate_cfg(cfg)) return rc;
+    DXRL_REQUIRE(out != nullptr, "null layout");
+    return layout_for(cfg, out);
+}
+
+int dxrl_env_create(const dxrl_env_config* cfg, int32_t device, void* state, void* stream, dxrl_env** out) {
+    if (int rc = validate_cfg(cfg)) return rc;
+    DXRL_REQUIRE(state != nullptr && out != nullptr, "null state/out");
+    DXRL_REQUIRE((reinterpret_cast<uintptr_t>(state) & 255) == 0, "state slab must be 256-byte aligned");
+    dxrl_env* e = new (std::nothrow) dxrl_env();
+    if (!e) {
+        set_error("host allocation failed");
+        return DXRL_E_INVALID;
+    }
+    e->cfg = *cfg;
+    e->device = device;
+    layout_for(cfg, &e->layout);
+    e->base = static_cast<char*>(state);
+    const dxrl_env_layout& L = e->layout;
+    char* b = e->base;
+    e->curricula = reinterpret_cast<dxrl_curriculum*>(b + L.curricula);
+    e->soa = EnvSoA{reinterpret_cast<float*>(b + L.jp),       reinterpret_cast<float*>(b + L.jv),
+                    reinterpret_cast<double*>(b + L.op),      reinterpret_cast<float*>(b + L.ov),
+                    reinterpret_cast<uint32_t*>(b + L.flags), reinterpret_cast<int32_t*>(b + L.step_count),
+                    reinterpret_cast<double*>(b + L.size),    reinterpret_cast<double*>(b + L.mass),
+                    reinterpret_cast<double*>(b + L.friction), reinterpret_cast<int32_t*>(b + L.cfg_index),
+                    reinterpret_cast<uint64_t*>(b + L.reset_ctr), nullptr, e->curricula, cfg->num_envs};
+    e->n_curricula = 1;
+    DeviceGuard g(device);
+    const int64_t n = cfg->num_envs;
+    hipLaunchKernelGGL(k_init, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, as_stream(stream), e->soa,
+                       cfg->has_object_position, cfg->object_position[0], cfg->object_position[1],
+                       cfg->object_position[2]);
+    if (int rc = launch_check("k_init")) {
+        delete e;
+        return rc;
+    }
+    // default curriculum row 0 = CurriculumConfig() (experiments/config.py:24-42)
+    dxrl_curriculum def{};
+    def.object_size = 0.05;
+    def.object_mass = 0.1;
+    def.friction_coefficient = 0.5;
+    def.spawn_x_range[0] = -0.1, def.spawn_x_range[1] = 0.1;
+    def.spawn_y_range[0] = -0.1, def.spawn_y_range[1] = 0.1;
+    def.spawn_z_range[0] = 0.05, def.spawn_z_range[1] = 0.2;
+    if (int rc = hip_check(hipMemcpyAsync(e->curricula, &def, sizeof def, hipMemcpyHostToDevice, as_stream(stream)),
+                           "curriculum upload") | hip_check(hipStreamSynchronize(as_stream(stream)), "create sync")) {
+        delete e;
+        return rc;
+    }
+    *out = e;
+    return DXRL_OK;
+}
+
+int dxrl_env_destroy(dxrl_env* env) {
+    delete env;
+    return DXRL_OK;
+}
+
+int dxrl_env_set_curricula(dxrl_env* env, const dxrl_curriculum* table, int32_t n, const int32_t* env_index,
+                           void* stream) {
+    DXRL_REQUIRE(env && table, "null env/table");
+    DXRL_REQUIRE(n >= 1 && n <= DXRL_MAX_CURRICULA, "curriculum table size %d outside [1, %d]", n,
+                 DXRL_MAX_CURRICULA);
+    for (int k = 0; k < n; ++k) {
+        const dxrl_curriculum& c = table[k];
+        DXRL_REQUIRE(c.object_size > 0.0 || c.has_size_range, "curriculum row %d: object_size must be > 0", k);
+    }
+    if (env_index)
+        for (int64_t i = 0; i < env->cfg.num_envs; ++i)
+            DXRL_REQUIRE(env_index[i] >= 0 && env_index[i] < n, "env %lld: curriculum row %d out of range",
+                         (long long)i, env_index[i]);
+    DeviceGuard g(env->device);
+    hipStream_t st = as_stream(stream);
+    // synchronous copies: host arrays may be temporaries of the caller
+    if (int rc = hip_check(hipMemcpyAsync(env->curricula, table, sizeof(dxrl_curriculum) * n, hipMemcpyHostToDevice, st),
+                           "curricula upload"))
+        return rc;
+    if (env_index) {
+        if (int rc = hip_check(hipMemcpyAsync(env->soa.cfg, env_index, sizeof(int32_t) * env->cfg.num_envs,
+                                              hipMemcpyHostToDevice, st),
+                               "env index upload"))
+            return rc;
+    } else {
+        if (int rc = hip_check(hipMemsetAsync(env->soa.cfg, 0, sizeof(int32_t) * env->cfg.num_envs, st), "index zero"))
+            return rc;
+    }
+    if (int rc = hip_check(hipStreamSynchronize(st), "curricula sync")) return rc;
+    env->n_curricula = n;
+    return DXRL_OK;
+}
+
+int dxrl_env_reset(dxrl_env* env, const uint8_t* mask, const double* draws, float* obs, void* stream) {
+    DXRL_REQUIRE(env, "null env");
+    DeviceGuard g(env->device);
+    const int64_t n = env->cfg.num_envs;
+    hipLaunchKernelGGL(k_reset, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, as_stream(stream),
+                       env->soa, mask, draws, obs, env->cfg.seed, (int64_t)env->cfg.global_env_offset);
+    return launch_check("k_reset");
+}
+
+int dxrl_env_step(dxrl_env* env, const float* actions, float* obs, double* reward, uint8_t* terminated,
+                  uint8_t* truncated, double* components, void* stream) {
+    DXRL_REQUIRE(env && actions && reward && terminated && truncated, "null env/actions/reward/flags");
+    DXRL_REQUIRE((reinterpret_cast<uintptr_t>(actions) & 15) == 0 && (reinterpret_cast<uintptr_t>(obs) & 15) == 0,
+                 "actions/obs must be 16-byte aligned");
+    DeviceGuard g(env->device);
+    const int64_t n = env->cfg.num_envs;
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+    const Weights w = weights_of(env->cfg);
+    const bool dense = env->cfg.reward_type == DXRL_REWARD_DENSE;
+    hipStream_t st = as_stream(stream);
+    const int mes = env->cfg.max_episode_steps;
+    if (dense)
+        hipLaunchKernelGGL((k_step<true>), grid, dim3(kBlock), 0, st, env->soa, actions, obs, reward, terminated,
+                           truncated, components, w, mes);
+    else
+        hipLaunchKernelGGL((k_step<false>), grid, dim3(kBlock), 0, st, env->soa, actions, obs, reward, terminated,
+                           truncated, components, w, mes);
+    return launch_check("k_step");
+}
+
+int dxrl_env_set_max_episode_steps(dxrl_env* env, int32_t max_episode_steps) {
+    DXRL_REQUIRE(env, "null env");
+    env->cfg.max_episode_steps = max_episode_steps;
+    return DXRL_OK;
+}
+
+int dxrl_env_observe(dxrl_env* env, float* obs, void* stream) {
+    DXRL_REQUIRE(env && obs, "null env/obs");
+    DeviceGuard g(env->device);
+    const int64_t n = env->cfg.num_envs;
+    hipLaunchKernelGGL(k_observe, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, as_stream(stream),
+                       env->soa, obs);
+    return launch_check("k_observe");
+}
+
+}  // extern "C"

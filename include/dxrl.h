@@ -1,0 +1,197 @@
+/*
+ * dxrl.h -- C ABI of the MI355X-native vectorised manipulation-env hot path.
+ *
+ * Plain C: no torch / HIP types in the signatures.  Device buffers are
+ * passed as plain pointers (HBM addresses valid on the env's device); streams
+ * as `void*` (a hipStream_t, NULL = the device's null stream).  Every entry
+ * point returns DXRL_OK (0) or a negative status; dxrl_last_error() returns a
+ * thread-local message for the last failing call.  Calls on one handle are
+ * not thread-safe; kernels are stream-ordered and asynchronous.
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to the I2S9/dexterous-rl-manipulation checkout).
+ */
+#ifndef DXRL_H_
+#define DXRL_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DXRL_ABI_VERSION 1
+
+/* status codes */
+#define DXRL_OK 0
+#define DXRL_E_INVALID (-1)     /* bad argument (shape, null pointer, range)  -> ValueError   */
+#define DXRL_E_HIP (-2)         /* HIP runtime / launch failure               -> RuntimeError */
+#define DXRL_E_UNSUPPORTED (-3) /* configuration this build does not compile   -> ValueError   */
+#define DXRL_E_TAPE (-4)        /* a parity tape ran out (see dxrl_rollout_*)  -> RuntimeError */
+
+/* reward plugin selection: envs/manipulation_env.py:64-73 */
+#define DXRL_REWARD_SPARSE 0 /* rewards/reward_shaping.py:190-242 SparseReward  */
+#define DXRL_REWARD_DENSE 1  /* rewards/reward_shaping.py:12-187  RewardShaping */
+
+/* number of f64 slots of one reset draw record: joints + (size, mass, friction) + spawn xyz */
+#define DXRL_RESET_EXTRA 6
+#define DXRL_MAX_CURRICULA 256
+
+/* episode success rule of a rollout:
+ *   TRAINING   -- training/episode_utils.py:52   info.get("success", False) -> always 0
+ *   TERMINATED -- evaluation/evaluator.py:157, robustness_tests.py:303   success = terminated */
+#define DXRL_SUCCESS_TRAINING 0
+#define DXRL_SUCCESS_TERMINATED 1
+
+/* One curriculum configuration -- experiments/config.py:17-42 (CurriculumConfig).
+ * A range is used iff its has_* flag is set (config.py:44-84: one draw each,
+ * in the order size, mass, friction).  friction_is_f64_scalar reproduces the
+ * NumPy-2 promotion when the friction is a numpy.float64 (scheduler
+ * interpolation, experiments/curriculum_scheduler.py:90-139): the velocity
+ * damping multiply then runs in f64 (manipulation_env.py:215-216). */
+typedef struct dxrl_curriculum {
+    double object_size, object_mass, friction_coefficient;
+    double size_range[2], mass_range[2], friction_range[2];
+    double spawn_x_range[2], spawn_y_range[2], spawn_z_range[2];
+    int32_t has_size_range, has_mass_range, has_friction_range, friction_is_f64_scalar;
+} dxrl_curriculum;
+
+/* Constructor arguments -- envs/manipulation_env.py:24-34 (+ reward_shaping.py:14-25 weights). */
+typedef struct dxrl_env_config {
+    int32_t num_envs;          /* N envs on this device (shard)                 */
+    int32_t num_fingers;       /* manipulation_env.py:26 (this build: 5)         */
+    int32_t joints_per_finger; /* manipulation_env.py:27 (this build: 3)         */
+    int32_t max_episode_steps; /* manipulation_env.py:29                         */
+    int32_t reward_type;       /* DXRL_REWARD_*  (manipulation_env.py:31)        */
+    int32_t has_object_position; /* manipulation_env.py:28 object_position given */
+    double object_position[3];
+    double distance_weight, contact_weight, closure_weight, stability_weight;
+    uint64_t seed;             /* device RNG: env i keyed by (seed, global_env_offset + i) */
+    int64_t global_env_offset; /* first global env id of this shard (multi-GPU)  */
+} dxrl_env_config;
+
+/* Byte offsets (from the state base) of the struct-of-arrays env state in HBM. */
+typedef struct dxrl_env_layout {
+    int64_t total_bytes;
+    int64_t jp, jv;      /* f32 [D][N]  joint positions / velocities            */
+    int64_t op;          /* f64 [3][N]  object position                         */
+    int64_t ov;          /* f32 [3][N]  object velocity                         */
+    int64_t flags;       /* u32 [N]     contacts | prev<<8 | has_prev<<16 | op_is_f32<<17 | has_object<<18 */
+    int64_t step_count;  /* i32 [N]                                              */
+    int64_t size, mass, friction; /* f64 [N] current episode curriculum values  */
+    int64_t cfg_index;   /* i32 [N]     curriculum table row per env             */
+    int64_t reset_ctr;   /* u64 [N]     resets so far (device-RNG counter)       */
+    int64_t curricula;   /* dxrl_curriculum [DXRL_MAX_CURRICULA]                 */
+} dxrl_env_layout;
+
+typedef struct dxrl_env dxrl_env;
+
+int dxrl_abi_version(void);
+const char* dxrl_last_error(void);
+
+/* Layout of the state slab the caller allocates (device memory, 256-B aligned). */
+int dxrl_env_layout_for(const dxrl_env_config* cfg, dxrl_env_layout* out);
+
+/* Replaces DexterousManipulationEnv.__init__ (envs/manipulation_env.py:24-122).
+ * `state` = caller-owned device slab of layout.total_bytes on `device`.
+ * Initialises the SoA (zeros, has_object from cfg) on `stream`. */
+int dxrl_env_create(const dxrl_env_config* cfg, int32_t device, void* state, void* stream, dxrl_env** out);
+int dxrl_env_destroy(dxrl_env* env);
+
+/* Curriculum table + per-env row (host arrays; copied asynchronously).
+ * env_index == NULL -> every env uses row 0.  Takes effect at the next reset,
+ * as assigning env.curriculum_config does (evaluation/component_ablation.py:166). */
+int dxrl_env_set_curricula(dxrl_env* env, const dxrl_curriculum* table, int32_t n,
+                           const int32_t* env_index, void* stream);
+
+/* Replaces reset(seed, options) (envs/manipulation_env.py:124-182).
+ * mask   : device u8 [N] or NULL (all envs)
+ * draws  : device f64 [N][D+6] resolved reset draws (parity mode: the host
+ *          replays each env's gymnasium PCG64 stream), or NULL -> device Philox.
+ *          Slots: D joint uniforms, size, mass, friction, spawn x, y, z (a slot
+ *          is read only when the reference would draw it).
+ * obs    : device f32 [N][obs_dim] or NULL. */
+int dxrl_env_reset(dxrl_env* env, const uint8_t* mask, const double* draws, float* obs, void* stream);
+
+/* Replaces step(action) (envs/manipulation_env.py:184-252) incl. _update_contacts
+ * (:285-310), the reward plugin (rewards/reward_shaping.py:50-242),
+ * _check_termination (:332-336) and _get_observation (:254-264).
+ * actions f32 [N][D]; obs f32 [N][obs_dim] (nullable); reward f64 [N];
+ * terminated/truncated u8 [N]; components f64 [N][4] (nullable). */
+int dxrl_env_step(dxrl_env* env, const float* actions, float* obs, double* reward,
+                  uint8_t* terminated, uint8_t* truncated, double* components, void* stream);
+
+/* Recompute the observation of the current state (envs/manipulation_env.py:254-264). */
+int dxrl_env_observe(dxrl_env* env, float* obs, void* stream);
+
+/* Assigning env.max_episode_steps (read by training/episode_utils.py:38 and
+ * the truncation test manipulation_env.py:245). */
+int dxrl_env_set_max_episode_steps(dxrl_env* env, int32_t max_episode_steps);
+
+/* SimpleLearner.select_action / update for a batch of independent learners
+ * (policies/simple_learner.py:49-95), for callers that drive env.step()
+ * themselves (the Gymnasium facade).  gauss = f64 [N][D] standard normals
+ * (np.random.normal(0, s) == 0 + s * gauss); update applies to envs whose
+ * mask byte is set -- the host decides `reward > best_reward` because it owns
+ * the RNG stream whose consumption depends on it. */
+int dxrl_learner_select(int32_t device, int32_t num_envs, const void* learner_state, double exploration_noise,
+                        const double* gauss, float* actions, void* stream);
+int dxrl_learner_update(int32_t device, int32_t num_envs, void* learner_state, double learning_rate,
+                        double action_clip_range, const double* gauss, const double* reward, const uint8_t* mask,
+                        void* stream);
+
+/* ------------------------------------------------------------------------
+ * Fused rollout with per-env SimpleLearner hill-climbers
+ * (training/episode_utils.py:13-55 run_episode loop + policies/simple_learner.py:49-99).
+ * One launch runs `num_steps` env steps of every env, auto-resetting at
+ * episode end (terminated || truncated || step_count == max_steps) exactly as
+ * consecutive run_episode() calls do.  State stays in registers across steps.
+ * ------------------------------------------------------------------------ */
+typedef struct dxrl_learner_layout {
+    int64_t total_bytes;
+    int64_t mean;        /* f32 [D][N] mean_action                             */
+    int64_t best;        /* f64 [N]    best_reward                             */
+    int64_t ep_return;   /* f64 [N]    running total_reward of the open episode */
+    int64_t noise_ctr;   /* u64 [N]    device-RNG counter                      */
+} dxrl_learner_layout;
+
+typedef struct dxrl_learner_config {
+    double learning_rate;     /* simple_learner.py:27 */
+    double exploration_noise; /* :28 */
+    double action_clip_range; /* :29 */
+    uint64_t seed;            /* device RNG (Philox) key; the reference uses the global np.random */
+} dxrl_learner_config;
+
+typedef struct dxrl_rollout_io {
+    /* parity tapes (all NULL -> device Philox streams) */
+    const double* gauss;      /* f64 [N][gauss_stride] legacy-MT19937 gauss values per env  */
+    int64_t gauss_stride;
+    const double* reset_draws;/* f64 [N][reset_stride] consecutive reset records (D+6 each) */
+    int64_t reset_stride;
+    /* episode records (nullable), [N][record_cap] */
+    int32_t record_cap;
+    double* ep_return;
+    int32_t* ep_length;
+    uint8_t* ep_success;
+    int32_t* ep_end_step;     /* rollout step index at which the episode ended */
+    /* per-env outputs (nullable) */
+    int32_t* ep_count;        /* i32 [N] episodes finished in this call   */
+    int32_t* gauss_used;      /* i32 [N] tape values consumed             */
+    int32_t* status;          /* i32 [1] device error word (tape overrun) */
+} dxrl_rollout_io;
+
+int dxrl_learner_layout_for(int32_t num_envs, int32_t action_dim, dxrl_learner_layout* out);
+/* zero mean_action, best_reward = -inf, ep_return = 0 (SimpleLearner.__init__, simple_learner.py:45-47) */
+int dxrl_learner_init(int32_t device, int32_t num_envs, void* learner_state, void* stream);
+/* policy.reset() for every env: best_reward = -inf (simple_learner.py:97-99) and the
+ * open-episode return = 0 (run_episode starts a new episode, episode_utils.py:33-39). */
+int dxrl_learner_reset(int32_t device, int32_t num_envs, void* learner_state, const uint8_t* mask, void* stream);
+/* learner_state must have been laid out for env's num_envs. */
+int dxrl_rollout_simple(dxrl_env* env, void* learner_state, const dxrl_learner_config* lcfg,
+                        int32_t num_steps, int32_t max_steps, int32_t success_rule,
+                        const dxrl_rollout_io* io, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DXRL_H_ */

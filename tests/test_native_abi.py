@@ -1,0 +1,89 @@
+"""CPU checks of the C ABI: the library loads, exports every declared symbol,
+and the ctypes mirrors have the C struct layouts (gcc-compiled probe)."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dxrl.h")
+
+
+@pytest.fixture(scope="module")
+def native():
+    import dexterous_rl_manipulation_amd as d
+    from dexterous_rl_manipulation_amd import _native
+    if not os.path.exists(_native.LIB_PATH):
+        d.build.build_native()
+    return _native
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(dxrl_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_entry_points():
+    fns = declared_functions()
+    assert "dxrl_env_step" in fns and "dxrl_rollout_simple" in fns and len(fns) >= 15
+
+
+def test_library_exports_every_declared_symbol(native):
+    lib = native.lib()
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+    assert set(declared_functions()) <= set(native._SIGS), "ctypes signatures missing"
+    assert lib.dxrl_abi_version() == native.ABI_VERSION
+
+
+def test_invalid_config_reports_error(native):
+    cfg = native.EnvConfig()
+    cfg.num_envs, cfg.num_fingers, cfg.joints_per_finger, cfg.reward_type = 8, 4, 3, 1
+    lay = native.EnvLayout()
+    with pytest.raises(ValueError, match="num_fingers"):
+        native.call("dxrl_env_layout_for", C.byref(cfg), C.byref(lay))
+    cfg.num_fingers, cfg.num_envs = 5, 0
+    with pytest.raises(ValueError, match="num_envs"):
+        native.call("dxrl_env_layout_for", C.byref(cfg), C.byref(lay))
+
+
+def test_layout_is_aligned_and_sized(native):
+    cfg = native.EnvConfig()
+    cfg.num_envs, cfg.num_fingers, cfg.joints_per_finger, cfg.reward_type = 4099, 5, 3, 1
+    lay = native.EnvLayout()
+    native.call("dxrl_env_layout_for", C.byref(cfg), C.byref(lay))
+    offs = [getattr(lay, f) for f, _ in native.EnvLayout._fields_[1:]]
+    assert all(o % 256 == 0 for o in offs)
+    assert offs == sorted(offs)
+    assert lay.jv - lay.jp >= 4 * 15 * 4099 and lay.total_bytes > lay.curricula
+
+
+STRUCTS = ["dxrl_curriculum", "dxrl_env_config", "dxrl_env_layout", "dxrl_learner_layout", "dxrl_learner_config",
+           "dxrl_rollout_io"]
+
+
+def test_ctypes_struct_layouts_match_c(native):
+    mirror = {"dxrl_curriculum": native.Curriculum, "dxrl_env_config": native.EnvConfig,
+              "dxrl_env_layout": native.EnvLayout, "dxrl_learner_layout": native.LearnerLayout,
+              "dxrl_learner_config": native.LearnerConfig, "dxrl_rollout_io": native.RolloutIO}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
+    for s in STRUCTS:
+        lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
+        for f, _ in mirror[s]._fields_:
+            lines.append(f'printf("{s}.{f} %zu\\n", offsetof({s}, {f}));')
+    lines.append("return 0;}")
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "probe.c")
+        open(c, "w").write("\n".join(lines))
+        exe = os.path.join(d, "probe")
+        subprocess.run(["gcc", "-std=c99", "-o", exe, c], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = dict(line.split() for line in out if line)
+    for s in STRUCTS:
+        assert int(got[s]) == C.sizeof(mirror[s]), s
+        for f, _ in mirror[s]._fields_:
+            assert int(got[f"{s}.{f}"]) == getattr(mirror[s], f).offset, f"{s}.{f}"

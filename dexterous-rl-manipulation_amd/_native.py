@@ -88,6 +88,9 @@ _SIGS = {
     "dxrl_learner_update": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_double, C.c_double, _P, _P, _P, _P]),
     "dxrl_rollout_simple": (C.c_int, [_P, _P, C.POINTER(LearnerConfig), C.c_int32, C.c_int32, C.c_int32,
                                       C.POINTER(RolloutIO), _P]),
+    "dxrl_gemm_bf16": (C.c_int, [C.c_int32, _P, C.c_int64, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P,
+                                 C.c_int64, C.c_int32, _P, C.c_int64, _P, C.c_int64, _P, C.c_int64, _P, C.c_int64,
+                                 C.c_int32, _P, _P]),
 }
 
 _lib = None

@@ -1,0 +1,43 @@
+// dxrl_mfma.h -- bf16 MFMA tiles for the actor-critic MLP (gfx950).
+//
+// All matrices are K-contiguous: A[m][k] (activations, row-major) and
+// Bt[n][k] (weights stored [out][in] like a torch Linear).  With that layout
+// both MFMA operand fragments of v_mfma_f32_32x32x16_bf16 are one 16-byte
+// load per lane: lane l (r = l & 31, h = l >> 5) holds A[r][8h..8h+7] and
+// Bt[r][8h..8h+7] (cdna_hip_programming.md §3 fragment layout).  The f32
+// accumulator of a 32x32 tile: col = l & 31, row = (reg & 3) + 8 (reg >> 2) + 4 h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dxrl {
+
+typedef __bf16 bf16;
+typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16 to_bf16(float x) { return (bf16)x; }  // v_cvt_pk_bf16_f32 (RNE)
+__device__ __forceinline__ float from_bf16(bf16 x) { return (float)x; }
+
+__device__ __forceinline__ int acc_row(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
+
+// Zero-filled 16-byte fragment load (rows >= rows_valid read as zero).
+__device__ __forceinline__ bf16x8 load_frag(const bf16* base, int64_t ld, int64_t row, int64_t rows_valid, int k) {
+    if (row < rows_valid) return *reinterpret_cast<const bf16x8*>(base + row * ld + k);
+    bf16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = (bf16)0.0f;
+    return z;
+}
+
+__device__ __forceinline__ float tanh_f(float x) {
+    // tanh via exp: 1 - 2 / (exp(2x) + 1); saturates cleanly for |x| large
+    const float e = __expf(2.0f * x);
+    return 1.0f - 2.0f / (e + 1.0f);
+}
+
+}  // namespace dxrl

@@ -191,6 +191,19 @@ int dxrl_rollout_simple(dxrl_env* env, void* learner_state, const dxrl_learner_c
                         int32_t num_steps, int32_t max_steps, int32_t success_rule,
                         const dxrl_rollout_io* io, void* stream);
 
+/* ------------------------------------------------------------------------
+ * bf16 MFMA GEMM used by the actor-critic learner (no reference counterpart;
+ * exported for tests and diagnostics).  C[M][N] = epi(A[M][K] . Bt[N][K]^T):
+ * bias (bias[n*bias_stride]), act (0 identity / 1 tanh), gate (multiply by
+ * 1 - gate[m][n]^2), outputs f32 row-major Cf, bf16 row-major Crm, bf16
+ * feature-major Cfm[n][m] (each nullable).  splits > 1: split-K over K into
+ * `partial` (f32 [splits][M][N]) reduced into Cf (ld = N).  K % 32 == 0.
+ * ------------------------------------------------------------------------ */
+int dxrl_gemm_bf16(int32_t device, const void* A, int64_t lda, const void* Bt, int64_t ldb, int64_t M, int32_t N,
+                   int32_t K, const float* bias, int64_t bias_stride, int32_t act, const void* gate, int64_t ldg,
+                   float* Cf, int64_t ldcf, void* Crm, int64_t ldc, void* Cfm, int64_t ldfm, int32_t splits,
+                   float* partial, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

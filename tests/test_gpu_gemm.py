@@ -1,0 +1,82 @@
+"""bf16 MFMA GEMM vs a plain torch fp32 reference of the same op.
+Tolerance: inputs are bf16 (exact in fp32), accumulation fp32 -> the only
+differences are fp32 summation order (rtol 1e-5 scale) and the bf16 rounding
+of bf16 outputs (rel 2^-8)."""
+import ctypes as C
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def N():
+    import dexterous_rl_manipulation_amd  # noqa: F401
+    from dexterous_rl_manipulation_amd import _native
+    return _native
+
+
+def gemm(N, A, Bt, *, bias=None, bias_stride=1, act=0, gate=None, out_f32=True, out_rm=False, out_fm=False,
+         splits=1):
+    M, K = A.shape
+    Nn = Bt.shape[0]
+    dev = A.device
+    Cf = torch.zeros(M, Nn, dtype=torch.float32, device=dev) if out_f32 else None
+    Crm = torch.zeros(M, Nn, dtype=torch.bfloat16, device=dev) if out_rm else None
+    Cfm = torch.zeros(Nn, M, dtype=torch.bfloat16, device=dev) if out_fm else None
+    partial = torch.empty(splits, M, Nn, dtype=torch.float32, device=dev) if splits > 1 else None
+    p = N.ptr
+    N.call("dxrl_gemm_bf16", dev.index, p(A), A.stride(0), p(Bt), Bt.stride(0), M, Nn, K, p(bias), bias_stride, act,
+           p(gate), 0 if gate is None else gate.stride(0), p(Cf), Nn, p(Crm), Nn, p(Cfm), M, splits, p(partial),
+           N.stream_of(dev))
+    torch.cuda.synchronize()
+    return Cf, Crm, Cfm
+
+
+@pytest.mark.parametrize("M,Nn,K", [(128, 128, 32), (300, 256, 64), (4096, 256, 256), (77, 32, 288), (1000, 288, 96)])
+def test_gemm_plain(N, M, Nn, K):
+    g = torch.Generator(device="cuda").manual_seed(M + Nn + K)
+    A = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    Bt = torch.randn(Nn, K, device="cuda", generator=g).to(torch.bfloat16)
+    Cf, _, _ = gemm(N, A, Bt)
+    ref = A.float() @ Bt.float().T
+    torch.testing.assert_close(Cf, ref, rtol=1e-5, atol=1e-4 * K ** 0.5)
+
+
+def test_gemm_asymmetric_identity(N):
+    """A = I with an asymmetric B catches a row/col swap in the C write."""
+    M = K = 64
+    A = torch.eye(M, K, device="cuda").to(torch.bfloat16)
+    Bt = (torch.arange(96 * K, device="cuda").reshape(96, K) % 251).float().to(torch.bfloat16)
+    Cf, _, _ = gemm(N, A, Bt)
+    torch.testing.assert_close(Cf, Bt.float().T[:M], rtol=0, atol=0)
+
+
+def test_gemm_epilogue_bias_tanh_gate_layouts(N):
+    M, Nn, K = 333, 256, 64
+    g = torch.Generator(device="cuda").manual_seed(3)
+    A = (0.3 * torch.randn(M, K, device="cuda", generator=g)).to(torch.bfloat16)
+    W = (0.3 * torch.randn(Nn, K + 8, device="cuda", generator=g)).to(torch.bfloat16)  # ld = K + 8
+    bias_mat = torch.randn(Nn, 3, device="cuda", generator=g)  # strided bias column
+    gate = torch.tanh(torch.randn(M, Nn, device="cuda", generator=g)).to(torch.bfloat16)
+    Cf, Crm, Cfm = gemm(N, A, W[:, :K], bias=bias_mat[:, 1], bias_stride=3, act=1, gate=gate, out_rm=True,
+                        out_fm=True)
+    ref = torch.tanh(A.float() @ W[:, :K].float().T + bias_mat[:, 1]) * (1 - gate.float() ** 2)
+    torch.testing.assert_close(Cf, ref, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(Crm.float(), ref, rtol=2 ** -7, atol=1e-6)
+    torch.testing.assert_close(Cfm.float().T, Crm.float(), rtol=0, atol=0)
+
+
+def test_gemm_split_k_weight_gradient_shape(N):
+    """dW[o][i] = sum_m dY[m][o] X[m][i] with both operands feature-major
+    (K = samples), split-K partial slabs reduced in fixed order."""
+    Ms, O, I = 40000, 256, 288
+    g = torch.Generator(device="cuda").manual_seed(9)
+    dYfm = (0.1 * torch.randn(O, Ms, device="cuda", generator=g)).to(torch.bfloat16)
+    Xfm = torch.randn(I, Ms, device="cuda", generator=g).to(torch.bfloat16)
+    Cf, _, _ = gemm(N, dYfm, Xfm, splits=13)
+    ref = dYfm.float() @ Xfm.float().T
+    torch.testing.assert_close(Cf, ref, rtol=1e-4, atol=2e-3)
+    Cf2, _, _ = gemm(N, dYfm, Xfm, splits=13)
+    assert torch.equal(Cf, Cf2)  # deterministic

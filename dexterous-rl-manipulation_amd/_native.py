@@ -69,7 +69,23 @@ class RolloutIO(C.Structure):
                 ("ep_count", C.c_void_p), ("gauss_used", C.c_void_p), ("status", C.c_void_p)]
 
 
+class PgRolloutArgs(C.Structure):
+    _fields_ = [("horizon", C.c_int32), ("max_steps", C.c_int32), ("policy_seed", C.c_uint64),
+                ("iteration", C.c_uint64), ("obs_noise_std", C.c_double), ("dyn_noise_std", C.c_double)] + \
+               [(k, C.c_void_p) for k in ("obs_rm", "obs_fm", "act", "logp", "rew", "done", "ep_return", "ep_count",
+                                          "ep_sum_return", "ep_sum_length", "ep_successes")]
+
+
+class PgHeadsArgs(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("mu", "values", "act", "logp_old", "adv", "ret", "stats", "params")] + \
+               [("num_samples", C.c_int64), ("inv_total_samples", C.c_double), ("clip_eps", C.c_double),
+                ("vf_coef", C.c_double), ("ent_coef", C.c_double)] + \
+               [(k, C.c_void_p) for k in ("dmu_rm", "dmu_fm", "dv_rm", "dv_fm", "dlogstd_partial", "loss_partial",
+                                          "grads")]
+
+
 _P = C.c_void_p
+_I32, _I64, _F64 = C.c_int32, C.c_int64, C.c_double
 _SIGS = {
     "dxrl_abi_version": (C.c_int, []),
     "dxrl_last_error": (C.c_char_p, []),
@@ -88,9 +104,16 @@ _SIGS = {
     "dxrl_learner_update": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_double, C.c_double, _P, _P, _P, _P]),
     "dxrl_rollout_simple": (C.c_int, [_P, _P, C.POINTER(LearnerConfig), C.c_int32, C.c_int32, C.c_int32,
                                       C.POINTER(RolloutIO), _P]),
-    "dxrl_gemm_bf16": (C.c_int, [C.c_int32, _P, C.c_int64, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P,
-                                 C.c_int64, C.c_int32, _P, C.c_int64, _P, C.c_int64, _P, C.c_int64, _P, C.c_int64,
-                                 C.c_int32, _P, _P]),
+    "dxrl_gemm_bf16": (C.c_int, [_I32, _P, _I64, _P, _I64, _I64, _I32, _I32, _P, _I64, _I32, _P, _I64, _P, _I64,
+                                 _P, _I64, _P, _I64, _P, _I64, _I32, _P, _P]),
+    "dxrl_pg_sizes": (C.c_int, [C.POINTER(_I64), C.POINTER(_I64)]),
+    "dxrl_pg_pack_weights": (C.c_int, [_I32, _P, _P, _P]),
+    "dxrl_pg_rollout": (C.c_int, [_P, _P, _P, C.POINTER(PgRolloutArgs), _P]),
+    "dxrl_pg_gae": (C.c_int, [_I32, _P, _P, _P, _I64, _I64, _F64, _F64, _P, _P, _P, _P, _P]),
+    "dxrl_pg_adv_finalize": (C.c_int, [_I32, _I32, _P, _I64, _P, _P, _P]),
+    "dxrl_pg_heads": (C.c_int, [_I32, C.POINTER(PgHeadsArgs), _P]),
+    "dxrl_pg_grad_sumsq": (C.c_int, [_I32, _P, _I64, _P, _P, _P]),
+    "dxrl_pg_adam": (C.c_int, [_I32, _P, _P, _P, _P, _I64, _F64, _F64, _F64, _F64, _I64, _P, _F64, _P]),
 }
 
 _lib = None

@@ -1,0 +1,36 @@
+// dxrl_gemm.h -- bf16 MFMA GEMM launcher shared by the learner kernels.
+#pragma once
+#include "dxrl_internal.h"
+#include "dxrl_mfma.h"
+
+namespace dxrl {
+
+struct GemmArgs {
+    const bf16* A;
+    int64_t lda;
+    const bf16* Bt;
+    int64_t ldb;
+    int64_t M;
+    int N, K;
+    int64_t k_chunk;        // split-K: K range per blockIdx.z (multiple of 32)
+    const float* bias;      // bias[n * bias_stride] (nullable)
+    int64_t bias_stride;
+    int act;                // 0 identity, 1 tanh
+    const bf16* gate;       // (1 - gate[m][n]^2) multiplier (tanh'), nullable
+    int64_t ldg;
+    float* Cf;              // f32 row-major out (nullable)
+    int64_t ldcf;
+    bf16* Crm;              // bf16 row-major out (nullable)
+    int64_t ldc;
+    bf16* Cfm;              // bf16 feature-major out Cfm[n][m] (nullable)
+    int64_t ldfm;
+    float* partial;         // split-K partial slab [z][M][N] f32 (nullable -> epilogue)
+    float* Cffm;            // f32 feature-major out Cffm[n][m] (nullable)
+    int64_t ldffm;
+};
+
+// Launch C = epi(A . Bt^T); splits > 1 -> split-K partial slabs reduced into
+// reduce_out (f32 [M][N], += when accumulate).
+int launch_gemm(const GemmArgs& g, int splits, float* reduce_out, int accumulate, hipStream_t st);
+
+}  // namespace dxrl

@@ -8,33 +8,11 @@
 // the weight operand is L2-resident (<= 150 KB per matrix), activations
 // stream once per column block.
 #include "dxrl_internal.h"
-#include "dxrl_mfma.h"
+#include "dxrl_gemm.h"
 
 using namespace dxrl;
 
 namespace dxrl {
-
-struct GemmArgs {
-    const bf16* A;
-    int64_t lda;
-    const bf16* Bt;
-    int64_t ldb;
-    int64_t M;
-    int N, K;
-    int64_t k_chunk;        // split-K: K range per blockIdx.z (multiple of 32)
-    const float* bias;      // bias[n * bias_stride] (nullable)
-    int64_t bias_stride;
-    int act;                // 0 identity, 1 tanh
-    const bf16* gate;       // (1 - gate[m][n]^2) multiplier (tanh'), nullable
-    int64_t ldg;
-    float* Cf;              // f32 row-major out (nullable)
-    int64_t ldcf;
-    bf16* Crm;              // bf16 row-major out (nullable)
-    int64_t ldc;
-    bf16* Cfm;              // bf16 feature-major out Cfm[n][m] (nullable)
-    int64_t ldfm;
-    float* partial;         // split-K partial slab [z][M][N] f32 (nullable -> epilogue)
-};
 
 constexpr int kWaveTile = 64, kBlockM = 128, kBlockN = 128;
 
@@ -96,6 +74,7 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(GemmArgs g) {
                     v = v * (1.0f - y * y);
                 }
                 if (g.Cf) g.Cf[m * g.ldcf + n] = v;
+                if (g.Cffm) g.Cffm[(int64_t)n * g.ldffm + m] = v;
                 const bf16 vb = to_bf16(v);
                 if (g.Crm) g.Crm[m * g.ldc + n] = vb;
                 if (g.Cfm) g.Cfm[(int64_t)n * g.ldfm + m] = vb;
@@ -146,12 +125,12 @@ extern "C" {
 // Test/diagnostic entry: C = epi(A . Bt^T) (see dxrl.h).
 int dxrl_gemm_bf16(int32_t device, const void* A, int64_t lda, const void* Bt, int64_t ldb, int64_t M, int32_t N,
                    int32_t K, const float* bias, int64_t bias_stride, int32_t act, const void* gate, int64_t ldg,
-                   float* Cf, int64_t ldcf, void* Crm, int64_t ldc, void* Cfm, int64_t ldfm, int32_t splits,
-                   float* partial, void* stream) {
+                   float* Cf, int64_t ldcf, void* Crm, int64_t ldc, void* Cfm, int64_t ldfm, float* Cffm,
+                   int64_t ldffm, int32_t splits, float* partial, void* stream) {
     DeviceGuard dg(device);
     GemmArgs g{static_cast<const bf16*>(A), lda, static_cast<const bf16*>(Bt), ldb, M, N, K, 0, bias, bias_stride,
                act, static_cast<const bf16*>(gate), ldg, Cf, ldcf, static_cast<bf16*>(Crm), ldc,
-               static_cast<bf16*>(Cfm), ldfm, splits > 1 ? partial : nullptr};
+               static_cast<bf16*>(Cfm), ldfm, splits > 1 ? partial : nullptr, Cffm, ldffm};
     return launch_gemm(g, splits, splits > 1 ? Cf : nullptr, 0, as_stream(stream));
 }
 

@@ -1,0 +1,629 @@
+// dxrl_pg.hip -- policy-gradient learner on MI355X (no reference counterpart:
+// the reference's only learner is the SimpleLearner hill-climber; SURVEY.md
+// §8(a) A11-A13).  Actor-critic MLP, GAE(gamma, lambda) reverse scan,
+// two-pass advantage normalisation, PPO-clip heads, Adam.
+//
+// k_pg_rollout is the hot loop: one workgroup owns 64 envs for the whole
+// horizon.  Per env step it runs the actor MLP on its 64-row tile with bf16
+// MFMA (weights streamed from L2, activations in LDS), samples
+// a = mu + sigma * eps (Philox), optionally injects dynamics / observation
+// noise (robustness_tests.py:140-211, config C5), steps the 64 envs (the
+// same env_step as dxrl_env_step), writes the training tape and auto-resets.
+// No inter-workgroup communication: envs and weights are independent/read-only.
+#include "dxrl_gemm.h"
+#include "dxrl_pg.h"
+
+using namespace dxrl;
+using namespace dxrl::pg;
+
+namespace dxrl {
+
+constexpr float kLog2Pi = 1.8378770664093453f;
+
+// log N(a | mu, sigma) summed over the action dims
+__device__ __forceinline__ float gauss_logp(const float* a, const float* mu, const float* logstd) {
+    float lp = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kAct; ++k) {
+        const float z = (a[k] - mu[k]) * __expf(-logstd[k]);
+        lp += -0.5f * z * z - logstd[k] - 0.5f * kLog2Pi;
+    }
+    return lp;
+}
+
+// 15 (or more) standard normals from one Philox stream position
+template <int N>
+__device__ __forceinline__ void philox_normals(float* out, uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream) {
+#pragma unroll
+    for (int b = 0; b < (N + 3) / 4; ++b) {
+        const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)b}, k0, k1);
+        float n0, n1, n2, n3;
+        box_muller(r.x, r.y, n0, n1);
+        box_muller(r.z, r.w, n2, n3);
+        if (4 * b + 0 < N) out[4 * b + 0] = n0;
+        if (4 * b + 1 < N) out[4 * b + 1] = n1;
+        if (4 * b + 2 < N) out[4 * b + 2] = n2;
+        if (4 * b + 3 < N) out[4 * b + 3] = n3;
+    }
+}
+
+struct PgRolloutArgs {
+    EnvSoA s;
+    Weights w;
+    int max_episode_steps, max_steps, horizon;
+    const bf16* wbf;
+    const float* params;
+    uint64_t env_seed, policy_seed;
+    int64_t gid0;
+    uint64_t iteration;
+    float obs_noise, dyn_noise;
+    bf16* obs_rm;   // [(T+1) N][kIn]
+    bf16* obs_fm;   // [kIn][T N]
+    float* act;     // [T N][kActPad]
+    float* logp;    // [T N]
+    float* rew;     // [T N]
+    uint8_t* done;  // [T N]
+    double* ep_ret; // [N] open-episode return (persists across calls)
+    int32_t* ep_count;
+    double* ep_sum_ret;
+    int32_t* ep_sum_len;
+    int32_t* ep_succ;
+};
+
+constexpr int kTile = 64;           // envs per workgroup
+constexpr int kXs = kIn + 8;        // LDS row strides (bf16) -- conflict-free b128 fragment reads
+constexpr int kHs = kH + 8;
+
+__device__ __forceinline__ void write_policy_obs(const Env& e, bf16* xrow, float obs_noise, uint32_t k0, uint32_t k1,
+                                                 uint64_t ctr, bf16* tape_rm, bf16* tape_fm, int64_t m,
+                                                 int64_t ld_fm) {
+    float o[kObs];
+    write_obs(e, o);
+    if (obs_noise > 0.0f) {  // robustness_tests.py:199-207, obs + f32(N(0, s))
+        float n[kObs];
+        philox_normals<kObs>(n, k0, k1, ctr, kStreamObs);
+#pragma unroll
+        for (int k = 0; k < kObs; ++k) o[k] = o[k] + obs_noise * n[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) xrow[k] = to_bf16(o[k]);
+    if (tape_rm) {
+        bf16x8 v[kIn / 8];
+#pragma unroll
+        for (int k = 0; k < kIn; ++k) v[k >> 3][k & 7] = k < kObs ? xrow[k] : (k == kObsIn ? (bf16)1.0f : (bf16)0.0f);
+#pragma unroll
+        for (int q = 0; q < kIn / 8; ++q) reinterpret_cast<bf16x8*>(tape_rm + m * kIn)[q] = v[q];
+    }
+    if (tape_fm) {
+#pragma unroll
+        for (int k = 0; k < kObs; ++k) tape_fm[(int64_t)k * ld_fm + m] = xrow[k];
+    }
+}
+
+// One wave computes a 64-row x 64-col output block of act(A . W^T + b) into LDS.
+// A: LDS [64][lda] bf16; W: global [n][ldw] rows n0..n0+63; K multiple of 16.
+// bias: f32 master column (bias[n * ldb]) -- the same values the training GEMMs use.
+template <int K, bool kTanh>
+__device__ __forceinline__ void wave_layer(const bf16* A, int lda, const bf16* W, int ldw, int n0, const float* bias_p,
+                                           int ldb, bf16* out, int ldo, int lane) {
+    const int r = lane & 31, h = lane >> 5;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.0f;
+#pragma unroll 4
+    for (int k = 0; k < K; k += 16) {
+        bf16x8 a[2], b[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const bf16x8*>(A + (32 * i + r) * lda + k + 8 * h);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            b[j] = *reinterpret_cast<const bf16x8*>(W + (int64_t)(n0 + 32 * j + r) * ldw + k + 8 * h);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = n0 + 32 * j + r;
+        const float bias = bias_p ? bias_p[(int64_t)n * ldb] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                float v = acc[i][j][q] + bias;
+                if (kTanh) v = tanh_f(v);
+                out[(32 * i + acc_row(q, lane)) * ldo + (n - n0)] = to_bf16(v);
+            }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pg_rollout(PgRolloutArgs p) {
+    __shared__ __attribute__((aligned(16))) bf16 X[kTile * kXs];
+    __shared__ __attribute__((aligned(16))) bf16 H1[kTile * kHs];
+    __shared__ __attribute__((aligned(16))) bf16 H2[kTile * kHs];
+    __shared__ __attribute__((aligned(16))) float MU[kTile * (kOut + 1)];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t n = p.s.n;
+    const int64_t i = (int64_t)blockIdx.x * kTile + lane;  // env of this lane (wave 0)
+    const bool live = i < n;
+    const int64_t T = p.horizon;
+    const bf16* W1 = p.wbf + kBfW1a;
+    const bf16* W2 = p.wbf + kBfW2a;
+    const bf16* W3 = p.wbf + kBfW3a;
+    Env e;
+    float logstd[kAct];
+    double ep_ret = 0.0;
+    int32_t cnt = 0, sum_len = 0, succ = 0;
+    double sum_ret = 0.0;
+    uint32_t ek0 = 0, ek1 = 0, pk0 = 0, pk1 = 0;
+    uint64_t rctr = 0;
+    if (wave == 0) {
+#pragma unroll
+        for (int k = 0; k < kAct; ++k) logstd[k] = p.params[kOffLogStd + k];
+        // constant padding of the X tile: bias column, zeros
+        for (int k = kObs; k < kIn; ++k) X[lane * kXs + k] = k == kObsIn ? (bf16)1.0f : (bf16)0.0f;
+        if (live) {
+            load_env(p.s, i, e);
+            ep_ret = p.ep_ret[i];
+            rctr = p.s.reset_ctr[i];
+            env_key(p.env_seed, p.gid0 + i, ek0, ek1);
+            env_key(p.policy_seed, p.gid0 + i, pk0, pk1);
+        } else {
+            for (int k = 0; k < kObs; ++k) X[lane * kXs + k] = (bf16)0.0f;
+        }
+    }
+    for (int64_t t = 0; t < T; ++t) {
+        const int64_t m = t * n + i;
+        const uint64_t ctr = p.iteration * (uint64_t)T + (uint64_t)t;
+        if (wave == 0 && live)
+            write_policy_obs(e, X + lane * kXs, p.obs_noise, pk0, pk1, ctr, p.obs_rm, p.obs_fm, m, T * n);
+        __syncthreads();
+        wave_layer<kIn, true>(X, kXs, W1, kIn, 64 * wave, nullptr, 0, H1 + 64 * wave, kHs, lane);  // bias = col 45
+        __syncthreads();
+        wave_layer<kH, true>(H1, kHs, W2, kHx, 64 * wave, p.params + kOffW2a + kH, kHx, H2 + 64 * wave, kHs, lane);
+        __syncthreads();
+        if (wave < 2) {  // mu head: rows 32*wave .. +31, 32 output columns
+            const int r = lane & 31, h = lane >> 5;
+            f32x16 acc;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+#pragma unroll 4
+            for (int k = 0; k < kH; k += 16) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHs + k + 8 * h);
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(W3 + (int64_t)r * kHx + k + 8 * h);
+                acc = mfma32(a, b, acc);
+            }
+            const float bias = p.params[kOffW3a + (int64_t)r * kHx + kH];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) MU[(32 * wave + acc_row(q, lane)) * (kOut + 1) + r] = acc[q] + bias;
+        }
+        __syncthreads();
+        if (wave == 0 && live) {
+            float mu[kAct], eps[kAct], a[kAct];
+#pragma unroll
+            for (int k = 0; k < kAct; ++k) mu[k] = MU[lane * (kOut + 1) + k];
+            philox_normals<kAct>(eps, pk0, pk1, ctr, kStreamPolicy);
+#pragma unroll
+            for (int k = 0; k < kAct; ++k) a[k] = mu[k] + __expf(logstd[k]) * eps[k];
+            p.logp[m] = gauss_logp(a, mu, logstd);
+            float4* arow = reinterpret_cast<float4*>(p.act + m * kActPad);
+            arow[0] = float4{a[0], a[1], a[2], a[3]};
+            arow[1] = float4{a[4], a[5], a[6], a[7]};
+            arow[2] = float4{a[8], a[9], a[10], a[11]};
+            arow[3] = float4{a[12], a[13], a[14], 0.0f};
+            float ae[kAct];
+            if (p.dyn_noise > 0.0f) {  // robustness_tests.py:180-187
+                float dn[kAct];
+                philox_normals<kAct>(dn, pk0, pk1, ctr, kStreamDyn);
+#pragma unroll
+                for (int k = 0; k < kAct; ++k) ae[k] = clipf(a[k] + p.dyn_noise * dn[k], -1.0f, 1.0f);
+            } else {
+#pragma unroll
+                for (int k = 0; k < kAct; ++k) ae[k] = a[k];
+            }
+            bool te, tr;
+            double cp[4];
+            const double r = env_step(e, ae, true, p.w, p.max_episode_steps, te, tr, cp);
+            ep_ret += r;
+            const bool d = te || tr || e.t >= p.max_steps;
+            p.rew[m] = (float)r;
+            p.done[m] = d;
+            if (d) {
+                ++cnt;
+                sum_ret += ep_ret;
+                sum_len += e.t;
+                succ += te;
+                const dxrl_curriculum cu = p.s.curricula[e.cfg];
+                double dr[kReset];
+                philox_reset_draws(dr, cu, ek0, ek1, rctr);
+                ++rctr;
+                env_reset(e, dr, cu);
+                ep_ret = 0.0;
+            }
+        }
+    }
+    if (wave == 0 && live) {
+        // bootstrap observation (slot T) -- with observation noise as the policy would see it
+        bf16 tmp[kObs];
+        const uint64_t ctr = p.iteration * (uint64_t)T + (uint64_t)T;
+        write_policy_obs(e, tmp, p.obs_noise, pk0, pk1, ctr, p.obs_rm, nullptr, T * n + i, 0);
+        store_env(p.s, i, e);
+        p.s.reset_ctr[i] = rctr;
+        p.ep_ret[i] = ep_ret;
+        p.ep_count[i] = cnt;
+        p.ep_sum_ret[i] = sum_ret;
+        p.ep_sum_len[i] = sum_len;
+        p.ep_succ[i] = succ;
+    }
+}
+
+// ------------------------------------------------------------------ GAE
+// delta_t = r_t + gamma V_{t+1} (1 - d_t) - V_t ; A_t = delta_t + gamma lambda (1 - d_t) A_{t+1}
+// One thread per env scans t = T-1 .. 0 (coalesced across envs).  Block
+// partial sums of A for the normalisation's first pass.
+__global__ void k_gae(const float* __restrict__ rew, const uint8_t* __restrict__ done, const float* __restrict__ V,
+                      int64_t n, int64_t T, float gamma, float lam, float* __restrict__ adv, float* __restrict__ ret,
+                      double* __restrict__ partial) {
+    __shared__ double red[256];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double s = 0.0;
+    if (i < n) {
+        float next_adv = 0.0f;
+        float next_v = V[T * n + i];
+        for (int64_t t = T - 1; t >= 0; --t) {
+            const int64_t m = t * n + i;
+            const float nd = done[m] ? 0.0f : 1.0f;
+            const float v = V[m];
+            const float delta = rew[m] + gamma * next_v * nd - v;
+            const float a = delta + gamma * lam * nd * next_adv;
+            adv[m] = a;
+            ret[m] = a + v;
+            s += a;
+            next_adv = a;
+            next_v = v;
+        }
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// block partials of sum (x - center)^2 (second pass of the normalisation)
+__global__ void k_sqdev(const float* __restrict__ x, int64_t count, const double* __restrict__ stats,
+                        double* __restrict__ partial) {
+    __shared__ double red[256];
+    const double c = stats[2];
+    double s = 0.0;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < count; k += (int64_t)gridDim.x * blockDim.x) {
+        const double d = (double)x[k] - c;
+        s += d * d;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// out[slot] = sum(partials) (fixed order)
+__global__ void k_sum_partials(const double* __restrict__ partial, int nb, double* __restrict__ out, int slot) {
+    __shared__ double red[256];
+    double s = 0.0;
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) s += partial[k];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[slot] = red[0];
+}
+
+// stats: [0] global count, [1] sum, [2] mean, [3] sum sq dev, [4] std
+__global__ void k_stats_mean(double* stats) { stats[2] = stats[1] / stats[0]; }
+__global__ void k_stats_std(double* stats) {
+    const double c = stats[0];
+    stats[4] = sqrt(stats[3] / (c > 1.0 ? c - 1.0 : 1.0));  // unbiased (torch.std)
+}
+
+// ------------------------------------------------------------------ PPO heads
+struct HeadArgs {
+    const float* mu;       // [M][kOut] f32 (actor head)
+    const float* V;        // [M] f32 (critic head row 0, feature-major)
+    const float* act;      // [M][kActPad]
+    const float* logp_old; // [M]
+    const float* adv;      // [M]
+    const float* ret;      // [M]
+    const double* stats;   // normalisation stats
+    const float* params;   // log_std
+    int64_t M;
+    double inv_total;      // 1 / global sample count (mean over all ranks)
+    float clip_eps, vf_coef;
+    bf16* dmu_rm;          // [M][kOut]
+    bf16* dmu_fm;          // [kOut][M]
+    bf16* dv_rm;           // [M][kOut] (col 0)
+    bf16* dv_fm;           // [kOut][M] (row 0)
+    float* dlogstd_partial;// [blocks][kActPad]
+    double* loss_partial;  // [blocks][4]: policy loss, value loss, clip fraction, approx kl
+};
+
+__global__ __launch_bounds__(256) void k_ppo_heads(HeadArgs h) {
+    __shared__ float red[256][kActPad];
+    __shared__ double lred[256][4];
+    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float dls[kAct];
+#pragma unroll
+    for (int k = 0; k < kAct; ++k) dls[k] = 0.0f;
+    double lp_loss = 0.0, lv = 0.0, clipped = 0.0, kl = 0.0;
+    if (m < h.M) {
+        float ls[kAct], mu[kAct], a[kAct];
+#pragma unroll
+        for (int k = 0; k < kAct; ++k) {
+            ls[k] = h.params[kOffLogStd + k];
+            mu[k] = h.mu[m * kOut + k];
+            a[k] = h.act[m * kActPad + k];
+        }
+        const float lp = gauss_logp(a, mu, ls);
+        const float ratio = __expf(lp - h.logp_old[m]);
+        const float A = (float)(((double)h.adv[m] - h.stats[2]) / (h.stats[4] + 1e-8));
+        const float s1 = ratio * A;
+        const float rc = fminf(fmaxf(ratio, 1.0f - h.clip_eps), 1.0f + h.clip_eps);
+        const float s2 = rc * A;
+        // d(-min(s1, s2))/d logp
+        float g = 0.0f;
+        if (s1 <= s2) g = -A * ratio;
+        else if (ratio == rc) g = -A * ratio;
+        const float sc = (float)h.inv_total;
+        g *= sc;
+#pragma unroll
+        for (int k = 0; k < kAct; ++k) {
+            const float iv = __expf(-2.0f * ls[k]);
+            const float d = a[k] - mu[k];
+            const float dmu = g * d * iv;              // dlogp/dmu = (a - mu) / sigma^2
+            dls[k] = g * (d * d * iv - 1.0f);          // dlogp/dlogstd = (a-mu)^2/sigma^2 - 1
+            h.dmu_rm[m * kOut + k] = to_bf16(dmu);
+            h.dmu_fm[(int64_t)k * h.M + m] = to_bf16(dmu);
+        }
+        const float v = h.V[m];
+        const float dv = 2.0f * h.vf_coef * (v - h.ret[m]) * sc;
+        h.dv_rm[m * kOut] = to_bf16(dv);
+        h.dv_fm[m] = to_bf16(dv);
+        lp_loss = -(double)fminf(s1, s2);
+        lv = (double)(v - h.ret[m]) * (double)(v - h.ret[m]);
+        clipped = fabsf(ratio - 1.0f) > h.clip_eps ? 1.0 : 0.0;
+        kl = (double)(h.logp_old[m] - lp);
+    }
+#pragma unroll
+    for (int k = 0; k < kAct; ++k) red[threadIdx.x][k] = dls[k];
+    lred[threadIdx.x][0] = lp_loss;
+    lred[threadIdx.x][1] = lv;
+    lred[threadIdx.x][2] = clipped;
+    lred[threadIdx.x][3] = kl;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+#pragma unroll
+            for (int k = 0; k < kAct; ++k) red[threadIdx.x][k] += red[threadIdx.x + w][k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) lred[threadIdx.x][k] += lred[threadIdx.x + w][k];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < kActPad)
+        h.dlogstd_partial[(int64_t)blockIdx.x * kActPad + threadIdx.x] = threadIdx.x < kAct ? red[0][threadIdx.x] : 0.0f;
+    if (threadIdx.x < 4) h.loss_partial[(int64_t)blockIdx.x * 4 + threadIdx.x] = lred[0][threadIdx.x];
+}
+
+// grads[kOffLogStd + k] = sum_b partial[b][k] - ent_coef  (entropy bonus: d(-c H)/d logstd = -c)
+__global__ void k_logstd_grad(const float* __restrict__ partial, int nb, float ent_coef, float* __restrict__ grads) {
+    const int k = threadIdx.x;
+    if (k >= kActPad) return;
+    float s = 0.0f;
+    for (int b = 0; b < nb; ++b) s += partial[(int64_t)b * kActPad + k];
+    grads[kOffLogStd + k] = k < kAct ? s - ent_coef : 0.0f;
+}
+
+// ------------------------------------------------------------------ optimiser
+// grad-norm^2 partials, then Adam with global-norm clipping (scale on device)
+__global__ void k_sumsq(const float* __restrict__ x, int64_t n, double* __restrict__ partial) {
+    __shared__ double red[256];
+    double s = 0.0;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        s += (double)x[k] * (double)x[k];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m1,
+                       float* __restrict__ m2, int64_t n, float lr, float b1, float b2, float eps, float bc1,
+                       float bc2, const double* __restrict__ gnorm2, float max_norm) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    float scale = 1.0f;
+    if (max_norm > 0.0f) {
+        const float nrm = (float)sqrt(gnorm2[0]);
+        scale = nrm > max_norm ? max_norm / (nrm + 1e-6f) : 1.0f;
+    }
+    const float gk = g[k] * scale;
+    const float a = b1 * m1[k] + (1.0f - b1) * gk;
+    const float b = b2 * m2[k] + (1.0f - b2) * gk * gk;
+    m1[k] = a;
+    m2[k] = b;
+    p[k] -= lr * (a / bc1) / (sqrtf(b / bc2) + eps);
+}
+
+// f32 master -> bf16 forward weights + transposed copies for input gradients
+__global__ void k_pack_weights(const float* __restrict__ p, bf16* __restrict__ w) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // forward copies (same layout as the master blocks)
+    if (k < kW1) {
+        w[kBfW1a + k] = to_bf16(p[kOffW1a + k]);
+        w[kBfW1c + k] = to_bf16(p[kOffW1c + k]);
+    }
+    if (k < kW2) {
+        w[kBfW2a + k] = to_bf16(p[kOffW2a + k]);
+        w[kBfW2c + k] = to_bf16(p[kOffW2c + k]);
+    }
+    if (k < kW3) {
+        w[kBfW3a + k] = to_bf16(p[kOffW3a + k]);
+        w[kBfW3c + k] = to_bf16(p[kOffW3c + k]);
+    }
+    if (k < kW2T) {  // W2T[i][o] = W2[o][i]
+        const int64_t i = k / kH, o = k % kH;
+        w[kBfW2aT + k] = to_bf16(p[kOffW2a + o * kHx + i]);
+        w[kBfW2cT + k] = to_bf16(p[kOffW2c + o * kHx + i]);
+    }
+    if (k < kW3T) {  // W3T[i][o] = W3[o][i]
+        const int64_t i = k / kOut, o = k % kOut;
+        w[kBfW3aT + k] = to_bf16(p[kOffW3a + o * kHx + i]);
+        w[kBfW3cT + k] = to_bf16(p[kOffW3c + o * kHx + i]);
+    }
+}
+
+static int reduce_to(const double* partial, int nb, double* out, int slot, hipStream_t st) {
+    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, partial, nb, out, slot);
+    return launch_check("k_sum_partials");
+}
+
+}  // namespace dxrl
+
+// =========================================================================== C ABI
+extern "C" {
+
+int dxrl_pg_sizes(int64_t* params, int64_t* packed_bf16) {
+    DXRL_REQUIRE(params && packed_bf16, "null outputs");
+    *params = kParams;
+    *packed_bf16 = kBf;
+    return DXRL_OK;
+}
+
+int dxrl_pg_pack_weights(int32_t device, const float* params, void* packed, void* stream) {
+    DXRL_REQUIRE(params && packed, "null params/packed");
+    DeviceGuard g(device);
+    const int64_t n = kW2 > kW2T ? kW2 : kW2T;  // largest block
+    hipLaunchKernelGGL(k_pack_weights, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), params,
+                       static_cast<bf16*>(packed));
+    return launch_check("k_pack_weights");
+}
+
+int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, const dxrl_pg_rollout_args* a,
+                    void* stream) {
+    DXRL_REQUIRE(env && packed && params && a, "null argument");
+    DXRL_REQUIRE(a->horizon > 0 && a->max_steps > 0, "horizon and max_steps must be > 0");
+    DXRL_REQUIRE(a->obs_rm && a->act && a->logp && a->rew && a->done && a->ep_return && a->ep_count &&
+                     a->ep_sum_return && a->ep_sum_length && a->ep_successes,
+                 "null tape / episode buffer");
+    DXRL_REQUIRE(env->cfg.reward_type == DXRL_REWARD_DENSE, "the policy-gradient rollout uses the dense reward");
+    PgRolloutArgs p{env->soa,
+                    weights_of(env->cfg),
+                    env->cfg.max_episode_steps,
+                    a->max_steps,
+                    a->horizon,
+                    static_cast<const bf16*>(packed),
+                    params,
+                    env->cfg.seed,
+                    a->policy_seed,
+                    env->cfg.global_env_offset,
+                    a->iteration,
+                    (float)a->obs_noise_std,
+                    (float)a->dyn_noise_std,
+                    static_cast<bf16*>(a->obs_rm),
+                    static_cast<bf16*>(a->obs_fm),
+                    a->act,
+                    a->logp,
+                    a->rew,
+                    a->done,
+                    a->ep_return,
+                    a->ep_count,
+                    a->ep_sum_return,
+                    a->ep_sum_length,
+                    a->ep_successes};
+    DeviceGuard g(env->device);
+    const int64_t n = env->cfg.num_envs;
+    hipLaunchKernelGGL(k_pg_rollout, dim3((unsigned)((n + kTile - 1) / kTile)), dim3(256), 0, as_stream(stream), p);
+    return launch_check("k_pg_rollout");
+}
+
+int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const float* values, int64_t num_envs,
+                int64_t horizon, double gamma, double lam, float* adv, float* ret, double* partial, double* stats,
+                void* stream) {
+    DXRL_REQUIRE(rew && done && values && adv && ret && partial && stats, "null argument");
+    DeviceGuard g(device);
+    hipStream_t st = as_stream(stream);
+    const int nb = (int)((num_envs + 255) / 256);
+    hipLaunchKernelGGL(k_gae, dim3(nb), dim3(256), 0, st, rew, done, values, num_envs, horizon, (float)gamma,
+                       (float)lam, adv, ret, partial);
+    if (int rc = launch_check("k_gae")) return rc;
+    return reduce_to(partial, nb, stats, 1, st);
+}
+
+int dxrl_pg_adv_finalize(int32_t device, int32_t phase, const float* adv, int64_t count, double* partial,
+                         double* stats, void* stream) {
+    DXRL_REQUIRE(adv && partial && stats, "null argument");
+    DeviceGuard g(device);
+    hipStream_t st = as_stream(stream);
+    if (phase == 0) {  // stats[1] (global sum) and stats[0] (global count) are set: mean, then sq-dev partials
+        hipLaunchKernelGGL(k_stats_mean, dim3(1), dim3(1), 0, st, stats);
+        if (int rc = launch_check("k_stats_mean")) return rc;
+        const int nb = 1024;
+        hipLaunchKernelGGL(k_sqdev, dim3(nb), dim3(256), 0, st, adv, count, stats, partial);
+        if (int rc = launch_check("k_sqdev")) return rc;
+        return reduce_to(partial, nb, stats, 3, st);
+    }
+    hipLaunchKernelGGL(k_stats_std, dim3(1), dim3(1), 0, st, stats);
+    return launch_check("k_stats_std");
+}
+
+int dxrl_pg_heads(int32_t device, const dxrl_pg_heads_args* a, void* stream) {
+    DXRL_REQUIRE(a, "null args");
+    DeviceGuard g(device);
+    HeadArgs h{a->mu, a->values, a->act, a->logp_old, a->adv, a->ret, a->stats, a->params, a->num_samples,
+               a->inv_total_samples, (float)a->clip_eps, (float)a->vf_coef,
+               static_cast<bf16*>(a->dmu_rm), static_cast<bf16*>(a->dmu_fm), static_cast<bf16*>(a->dv_rm),
+               static_cast<bf16*>(a->dv_fm), a->dlogstd_partial, a->loss_partial};
+    const int nb = (int)((a->num_samples + 255) / 256);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_ppo_heads, dim3(nb), dim3(256), 0, st, h);
+    if (int rc = launch_check("k_ppo_heads")) return rc;
+    hipLaunchKernelGGL(k_logstd_grad, dim3(1), dim3(64), 0, st, a->dlogstd_partial, nb, (float)a->ent_coef,
+                       a->grads);
+    return launch_check("k_logstd_grad");
+}
+
+int dxrl_pg_grad_sumsq(int32_t device, const float* grads, int64_t n, double* partial, double* out, void* stream) {
+    DeviceGuard g(device);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_sumsq, dim3(512), dim3(256), 0, st, grads, n, partial);
+    if (int rc = launch_check("k_sumsq")) return rc;
+    return reduce_to(partial, 512, out, 0, st);
+}
+
+int dxrl_pg_adam(int32_t device, float* params, const float* grads, float* m1, float* m2, int64_t n, double lr,
+                 double beta1, double beta2, double eps, int64_t step, const double* gnorm2, double max_norm,
+                 void* stream) {
+    DXRL_REQUIRE(params && grads && m1 && m2 && step >= 1, "bad adam arguments");
+    DeviceGuard g(device);
+    const float bc1 = (float)(1.0 - pow(beta1, (double)step)), bc2 = (float)(1.0 - pow(beta2, (double)step));
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), params, grads, m1,
+                       m2, n, (float)lr, (float)beta1, (float)beta2, (float)eps, bc1, bc2, gnorm2,
+                       (float)max_norm);
+    return launch_check("k_adam");
+}
+
+}  // extern "C"

@@ -1,0 +1,286 @@
+"""Vectorised policy-gradient trainer (NEW capability).
+
+The reference's learner is a per-episode random hill-climber
+(policies/simple_learner.py); BASELINE.json asks for an MLP(256,256)
+actor-critic with GAE and policy gradients on top of the same env.  One
+``PGTrainer.iteration()`` =
+
+  1. ``dxrl_pg_rollout``  -- T env steps of every env, actor MLP fused into
+     the step kernel (bf16 MFMA), Gaussian sampling, optional fused noise
+     injection (robustness_tests.py:140-211), auto-reset, training tape;
+  2. critic forward over the T+1 observation blocks (bf16 MFMA GEMMs);
+  3. ``dxrl_pg_gae`` reverse scan + two-pass advantage normalisation
+     (global across ranks: two 1-element all-reduces);
+  4. actor forward, PPO-clip / value / entropy heads (``dxrl_pg_heads``);
+  5. backward GEMMs (input grads with fused tanh' gate, weight grads by
+     split-K over samples with the bias as an extra ones-row);
+  6. one flat f32 gradient all-reduce over RCCL (world > 1);
+  7. global-norm clip + Adam on the f32 master, bf16 repack.
+
+Every matrix contraction runs in libdxrl.so; torch only owns the buffers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .envs import VecEnv
+
+# csrc/dxrl_pg.h
+OBS_IN, IN, H, HX, OUT, ACT, ACT_PAD = 45, 64, 256, 288, 32, 15, 16
+W1, W2, W3 = H * IN, H * HX, OUT * HX
+OFF = {"W1a": 0, "W2a": W1, "W3a": W1 + W2, "logstd": W1 + W2 + W3}
+OFF["W1c"] = OFF["logstd"] + 32
+OFF["W2c"] = OFF["W1c"] + W1
+OFF["W3c"] = OFF["W2c"] + W2
+NPARAMS = OFF["W3c"] + W3
+W2T, W3T = H * H, H * OUT
+BF = {"W1a": 0, "W2a": W1, "W3a": W1 + W2, "W2aT": W1 + W2 + W3, "W3aT": W1 + W2 + W3 + W2T}
+BF["W1c"] = BF["W3aT"] + W3T
+BF["W2c"] = BF["W1c"] + W1
+BF["W3c"] = BF["W2c"] + W2
+BF["W2cT"] = BF["W3c"] + W3
+BF["W3cT"] = BF["W2cT"] + W2T
+NBF = BF["W3cT"] + W3T
+LOGICAL_PARAMS = 2 * (OBS_IN * H + H) + 2 * (H * H + H) + (H * ACT + ACT) + (H + 1) + ACT  # 159,263
+
+
+@dataclass
+class TrainerConfig:
+    """Build-owned knobs (never stored in the reference's strict dataclasses)."""
+    horizon: int = 200
+    max_steps: Optional[int] = None          # run_episode loop bound; default env.max_episode_steps
+    gamma: float = 0.99
+    lam: float = 0.95
+    clip_eps: float = 0.2
+    vf_coef: float = 0.5
+    ent_coef: float = 0.0
+    lr: float = 3e-4
+    betas: tuple = (0.9, 0.999)
+    adam_eps: float = 1e-5
+    max_grad_norm: float = 0.5
+    init_log_std: float = -0.5
+    obs_noise_std: float = 0.0               # config C5: 0.05
+    dyn_noise_std: float = 0.0               # config C5: 0.05
+    seed: int = 0
+    splitk_target_blocks: int = 768
+
+
+class PGTrainer:
+    def __init__(self, env: VecEnv, cfg: TrainerConfig = TrainerConfig(), process_group=None, world_size: int = 1):
+        if env.reward_type != "dense":
+            raise ValueError("the policy-gradient trainer uses the dense reward")
+        p_, b_ = C.c_int64(), C.c_int64()
+        N.call("dxrl_pg_sizes", C.byref(p_), C.byref(b_))
+        assert (p_.value, b_.value) == (NPARAMS, NBF), "csrc/dxrl_pg.h and trainer.py disagree"
+        self.env, self.cfg = env, cfg
+        self.dev = env.device
+        self.n = env.num_envs
+        self.T = cfg.horizon
+        self.M = self.n * self.T
+        if self.M % 32:
+            raise ValueError("num_envs * horizon must be a multiple of 32")
+        self.max_steps = cfg.max_steps or env.max_episode_steps
+        self.pg = process_group
+        self.world = world_size
+        self.step_count = 0
+        self.iteration_index = 0
+        d, f32, bf, M, n, T = self.dev, torch.float32, torch.bfloat16, self.M, self.n, self.T
+        z = lambda *s, dt=f32: torch.zeros(*s, dtype=dt, device=d)  # noqa: E731
+        self.params, self.grads, self.m1, self.m2 = z(NPARAMS), z(NPARAMS), z(NPARAMS), z(NPARAMS)
+        self.packed = z(NBF, dt=bf)
+        self._init_params()
+        # tape
+        self.obs_rm = z((T + 1) * n, IN, dt=bf)
+        self.obs_fm = z(IN, M, dt=bf)
+        self.obs_fm[OBS_IN].fill_(1.0)
+        self.act = z(M, ACT_PAD)
+        self.logp, self.rew = z(M), z(M)
+        self.done = z(M, dt=torch.uint8)
+        self.ep_ret = torch.zeros(n, dtype=torch.float64, device=d)
+        self.ep_count = z(n, dt=torch.int32)
+        self.ep_sum_ret = torch.zeros(n, dtype=torch.float64, device=d)
+        self.ep_sum_len = z(n, dt=torch.int32)
+        self.ep_succ = z(n, dt=torch.int32)
+        # activations (row-major A operands / gates, feature-major weight-grad operands with a ones row)
+        self.H1a, self.H2a = z(M, H, dt=bf), z(M, H, dt=bf)
+        self.H1c, self.H2c = z((T + 1) * n, H, dt=bf), z((T + 1) * n, H, dt=bf)
+        self.H1a_fm, self.H2a_fm, self.H1c_fm, self.H2c_fm = (z(HX, M, dt=bf) for _ in range(4))
+        for t in (self.H1a_fm, self.H2a_fm, self.H1c_fm, self.H2c_fm):
+            t[H].fill_(1.0)
+        self.mu = z(M, OUT)
+        self.V = z(OUT, (T + 1) * n)
+        self.adv, self.ret = z(M), z(M)
+        self.stats = torch.zeros(8, dtype=torch.float64, device=d)
+        nb = max(1024, (M + 255) // 256, (n + 255) // 256)
+        self.partial = torch.zeros(nb, dtype=torch.float64, device=d)
+        self.dmu_rm, self.dmu_fm = z(M, OUT, dt=bf), z(OUT, M, dt=bf)
+        self.dv_rm, self.dv_fm = z(M, OUT, dt=bf), z(OUT, M, dt=bf)
+        self.dls_partial = z((M + 255) // 256, ACT_PAD)
+        self.loss_partial = torch.zeros((M + 255) // 256, 4, dtype=torch.float64, device=d)
+        self.dH2_rm, self.dH2_fm, self.dH1_fm = z(M, H, dt=bf), z(H, M, dt=bf), z(H, M, dt=bf)
+        self.splits = max(1, min(cfg.splitk_target_blocks // 6, M // 4096))
+        self.kpartial = z(self.splits, H, HX)
+        self.gnorm2 = torch.zeros(1, dtype=torch.float64, device=d)
+        self.pack()
+
+    # ------------------------------------------------------------------ params
+    def _view(self, t, off, rows, cols):
+        return t[off:off + rows * cols].view(rows, cols)
+
+    def block(self, name, t=None):
+        t = self.params if t is None else t
+        shape = {"W1": (H, IN), "W2": (H, HX), "W3": (OUT, HX)}[name[:2]]
+        return self._view(t, OFF[name], *shape)
+
+    def _init_params(self):
+        g = torch.Generator(device="cpu").manual_seed(int(self.cfg.seed))
+        for net, head_rows, head_gain in (("a", ACT, 0.01), ("c", 1, 1.0)):
+            for name, rows, cols, gain in ((f"W1{net}", H, OBS_IN, math.sqrt(2)), (f"W2{net}", H, H, math.sqrt(2)),
+                                           (f"W3{net}", head_rows, H, head_gain)):
+                w = torch.empty(rows, cols)
+                torch.nn.init.orthogonal_(w, gain=gain, generator=g)
+                self.block(name)[:rows, :cols].copy_(w.to(self.dev))
+        self.params[OFF["logstd"]:OFF["logstd"] + ACT].fill_(self.cfg.init_log_std)
+
+    def pack(self):
+        N.call("dxrl_pg_pack_weights", self.dev.index, N.ptr(self.params), N.ptr(self.packed), self._s())
+
+    def _s(self):
+        return N.stream_of(self.dev)
+
+    def _bf(self, name):
+        return self.packed[BF[name]:]
+
+    # ------------------------------------------------------------------ launches
+    def _gemm(self, A, lda, Bt, ldb, M, Nn, K, *, bias=None, bias_stride=0, act=0, gate=None, ldg=0, Cf=None,
+              ldcf=0, Crm=None, ldc=0, Cfm=None, ldfm=0, Cffm=None, ldffm=0, splits=1, partial=None):
+        p = N.ptr
+        N.call("dxrl_gemm_bf16", self.dev.index, p(A), lda, p(Bt), ldb, M, Nn, K, p(bias), bias_stride, act, p(gate),
+               ldg, p(Cf), ldcf, p(Crm), ldc, p(Cfm), ldfm, p(Cffm), ldffm, splits, p(partial), self._s())
+
+    def _wgrad(self, A_fm, Bt_fm, rows, cols, dst):
+        """dst[rows][cols] = A_fm[rows][M] . Bt_fm[cols][M]^T (split-K over samples)."""
+        self._gemm(A_fm, self.M, Bt_fm, self.M, rows, cols, self.M, Cf=dst, ldcf=cols, splits=self.splits,
+                   partial=self.kpartial)
+
+    def rollout(self):
+        a = N.PgRolloutArgs()
+        a.horizon, a.max_steps = self.T, self.max_steps
+        a.policy_seed = (int(self.cfg.seed) * 0x9E3779B97F4A7C15 + 17) & (2**64 - 1)
+        a.iteration = self.iteration_index
+        a.obs_noise_std, a.dyn_noise_std = self.cfg.obs_noise_std, self.cfg.dyn_noise_std
+        p = N.ptr
+        a.obs_rm, a.obs_fm, a.act, a.logp, a.rew, a.done = (p(self.obs_rm), p(self.obs_fm), p(self.act),
+                                                            p(self.logp), p(self.rew), p(self.done))
+        a.ep_return, a.ep_count, a.ep_sum_return = p(self.ep_ret), p(self.ep_count), p(self.ep_sum_ret)
+        a.ep_sum_length, a.ep_successes = p(self.ep_sum_len), p(self.ep_succ)
+        N.call("dxrl_pg_rollout", self.env.handle, p(self.packed), p(self.params), C.byref(a), self._s())
+
+    def critic_forward(self):
+        M, n, P = self.M, self.n, self.params
+        rows = M + n
+        # L1 (bias = column 45 of W1 against the constant-1 input): rows [0, M) also feature-major
+        self._gemm(self.obs_rm, IN, self._bf("W1c"), IN, M, H, IN, act=1, Crm=self.H1c, ldc=H, Cfm=self.H1c_fm,
+                   ldfm=M)
+        self._gemm(self.obs_rm[M:], IN, self._bf("W1c"), IN, n, H, IN, act=1, Crm=self.H1c[M:], ldc=H)
+        b2, b3 = P[OFF["W2c"] + H:], P[OFF["W3c"] + H:]
+        self._gemm(self.H1c, H, self._bf("W2c"), HX, M, H, H, bias=b2, bias_stride=HX, act=1, Crm=self.H2c,
+                   ldc=H, Cfm=self.H2c_fm, ldfm=M)
+        self._gemm(self.H1c[M:], H, self._bf("W2c"), HX, n, H, H, bias=b2, bias_stride=HX, act=1, Crm=self.H2c[M:],
+                   ldc=H)
+        self._gemm(self.H2c, H, self._bf("W3c"), HX, rows, OUT, H, bias=b3, bias_stride=HX, Cffm=self.V,
+                   ldffm=rows)
+
+    def actor_forward(self):
+        M, P = self.M, self.params
+        self._gemm(self.obs_rm, IN, self._bf("W1a"), IN, M, H, IN, act=1, Crm=self.H1a, ldc=H, Cfm=self.H1a_fm,
+                   ldfm=M)
+        self._gemm(self.H1a, H, self._bf("W2a"), HX, M, H, H, bias=P[OFF["W2a"] + H:], bias_stride=HX, act=1,
+                   Crm=self.H2a, ldc=H, Cfm=self.H2a_fm, ldfm=M)
+        self._gemm(self.H2a, H, self._bf("W3a"), HX, M, OUT, H, bias=P[OFF["W3a"] + H:], bias_stride=HX, Cf=self.mu,
+                   ldcf=OUT)
+
+    def _allreduce(self, t):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+
+    def advantages(self):
+        c = self.cfg
+        N.call("dxrl_pg_gae", self.dev.index, N.ptr(self.rew), N.ptr(self.done), N.ptr(self.V[0]), self.n, self.T,
+               c.gamma, c.lam, N.ptr(self.adv), N.ptr(self.ret), N.ptr(self.partial), N.ptr(self.stats), self._s())
+        self.stats[0] = float(self.M)
+        self._allreduce(self.stats[0:2])
+        N.call("dxrl_pg_adv_finalize", self.dev.index, 0, N.ptr(self.adv), self.M, N.ptr(self.partial),
+               N.ptr(self.stats), self._s())
+        self._allreduce(self.stats[3:4])
+        N.call("dxrl_pg_adv_finalize", self.dev.index, 1, N.ptr(self.adv), self.M, N.ptr(self.partial),
+               N.ptr(self.stats), self._s())
+
+    def heads(self):
+        c, p = self.cfg, N.ptr
+        h = N.PgHeadsArgs()
+        h.mu, h.values, h.act, h.logp_old = p(self.mu), p(self.V[0]), p(self.act), p(self.logp)
+        h.adv, h.ret, h.stats, h.params = p(self.adv), p(self.ret), p(self.stats), p(self.params)
+        h.num_samples = self.M
+        h.inv_total_samples = 1.0 / (self.M * self.world)
+        h.clip_eps, h.vf_coef, h.ent_coef = c.clip_eps, c.vf_coef, c.ent_coef / self.world
+        h.dmu_rm, h.dmu_fm, h.dv_rm, h.dv_fm = p(self.dmu_rm), p(self.dmu_fm), p(self.dv_rm), p(self.dv_fm)
+        h.dlogstd_partial, h.loss_partial, h.grads = p(self.dls_partial), p(self.loss_partial), p(self.grads)
+        N.call("dxrl_pg_heads", self.dev.index, C.byref(h), self._s())
+
+    def backward(self):
+        M, G = self.M, self.grads
+        for net, dY_rm, dY_fm, H1, H2, H1fm, H2fm in (
+                ("a", self.dmu_rm, self.dmu_fm, self.H1a, self.H2a, self.H1a_fm, self.H2a_fm),
+                ("c", self.dv_rm, self.dv_fm, self.H1c, self.H2c, self.H1c_fm, self.H2c_fm)):
+            self._wgrad(dY_fm, H2fm, OUT, HX, self.block(f"W3{net}", G))
+            self._gemm(dY_rm, OUT, self._bf(f"W3{net}T"), OUT, M, H, OUT, gate=H2, ldg=H, Crm=self.dH2_rm, ldc=H,
+                       Cfm=self.dH2_fm, ldfm=M)
+            self._wgrad(self.dH2_fm, H1fm, H, HX, self.block(f"W2{net}", G))
+            self._gemm(self.dH2_rm, H, self._bf(f"W2{net}T"), H, M, H, H, gate=H1, ldg=H, Cfm=self.dH1_fm, ldfm=M)
+            self._wgrad(self.dH1_fm, self.obs_fm, H, IN, self.block(f"W1{net}", G))
+
+    def optimizer_step(self):
+        c = self.cfg
+        self._allreduce(self.grads)
+        N.call("dxrl_pg_grad_sumsq", self.dev.index, N.ptr(self.grads), NPARAMS, N.ptr(self.partial),
+               N.ptr(self.gnorm2), self._s())
+        self.step_count += 1
+        N.call("dxrl_pg_adam", self.dev.index, N.ptr(self.params), N.ptr(self.grads), N.ptr(self.m1), N.ptr(self.m2),
+               NPARAMS, c.lr, c.betas[0], c.betas[1], c.adam_eps, self.step_count, N.ptr(self.gnorm2),
+               c.max_grad_norm, self._s())
+        self.pack()
+
+    def iteration(self, update: bool = True):
+        self.rollout()
+        self.critic_forward()
+        self.advantages()
+        self.actor_forward()
+        self.heads()
+        self.backward()
+        if update:
+            self.optimizer_step()
+        self.iteration_index += 1
+
+    # ------------------------------------------------------------------ stats
+    def episode_stats(self) -> Dict[str, float]:
+        cnt = int(self.ep_count.sum().item())
+        out = {"episodes": cnt, "env_steps": self.M}
+        if cnt:
+            out["mean_return"] = float(self.ep_sum_ret.sum().item()) / cnt
+            out["mean_length"] = float(self.ep_sum_len.sum().item()) / cnt
+            out["success_rate"] = float(self.ep_succ.sum().item()) / cnt
+        return out
+
+    def loss_stats(self) -> Dict[str, float]:
+        s = self.loss_partial.sum(0).cpu().numpy() / self.M
+        return {"policy_loss": float(s[0]), "value_mse": float(s[1]), "clip_frac": float(s[2]),
+                "approx_kl": float(s[3]), "grad_norm": float(np.sqrt(self.gnorm2.item()))}

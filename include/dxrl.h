@@ -201,8 +201,83 @@ int dxrl_rollout_simple(dxrl_env* env, void* learner_state, const dxrl_learner_c
  * ------------------------------------------------------------------------ */
 int dxrl_gemm_bf16(int32_t device, const void* A, int64_t lda, const void* Bt, int64_t ldb, int64_t M, int32_t N,
                    int32_t K, const float* bias, int64_t bias_stride, int32_t act, const void* gate, int64_t ldg,
-                   float* Cf, int64_t ldcf, void* Crm, int64_t ldc, void* Cfm, int64_t ldfm, int32_t splits,
-                   float* partial, void* stream);
+                   float* Cf, int64_t ldcf, void* Crm, int64_t ldc, void* Cfm, int64_t ldfm, float* Cffm,
+                   int64_t ldffm, int32_t splits, float* partial, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Policy-gradient learner (NEW capability: the reference has no network,
+ * no GAE and no gradient -- SURVEY.md §8(a) A11-A13; parity unpinned vs the
+ * reference, pinned by tests against a torch fp32 restatement).
+ * Actor 45->256->256->15 (tanh) + state-independent log_std; critic
+ * 45->256->256->1.  Master parameters f32 (dxrl_pg_sizes().params elements,
+ * padded blocks, see csrc/dxrl_pg.h), bf16 packed copies for the MFMA GEMMs.
+ * ------------------------------------------------------------------------ */
+int dxrl_pg_sizes(int64_t* params, int64_t* packed_bf16);
+int dxrl_pg_pack_weights(int32_t device, const float* params, void* packed, void* stream);
+
+typedef struct dxrl_pg_rollout_args {
+    int32_t horizon;           /* env steps per env in this call (T)                       */
+    int32_t max_steps;         /* run_episode loop bound (episode_utils.py:38-42)          */
+    uint64_t policy_seed;      /* Philox key of the action / noise streams                 */
+    uint64_t iteration;        /* Philox counter base (iteration * T + t)                  */
+    double obs_noise_std;      /* robustness_tests.py:199-207 (0 = off)                    */
+    double dyn_noise_std;      /* robustness_tests.py:180-187 (0 = off)                    */
+    void* obs_rm;              /* bf16 [(T+1) N][64] policy inputs (+ bootstrap row block) */
+    void* obs_fm;              /* bf16 [64][T N] feature-major copy (nullable)             */
+    float* act;                /* f32 [T N][16] sampled (pre-clip) actions                 */
+    float* logp;               /* f32 [T N] log pi(a|s) at sampling time                   */
+    float* rew;                /* f32 [T N]                                                */
+    uint8_t* done;             /* u8  [T N] episode ended after this step                  */
+    double* ep_return;         /* f64 [N] open-episode return, persists across calls       */
+    int32_t* ep_count;         /* i32 [N] episodes finished in this call                   */
+    double* ep_sum_return;     /* f64 [N]                                                  */
+    int32_t* ep_sum_length;    /* i32 [N]                                                  */
+    int32_t* ep_successes;     /* i32 [N] finished episodes that terminated (>= 3 contacts) */
+} dxrl_pg_rollout_args;
+
+/* Fused policy + env rollout: T steps of actor MLP (bf16 MFMA) -> Gaussian
+ * sample -> [dynamics noise] -> env step -> tape, auto-reset (device RNG). */
+int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, const dxrl_pg_rollout_args* args,
+                    void* stream);
+
+/* GAE reverse scan; values f32 [(T+1) N]; writes adv/ret [T N] and stats[1] = local sum(adv). */
+int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const float* values, int64_t num_envs,
+                int64_t horizon, double gamma, double lam, float* adv, float* ret, double* partial, double* stats,
+                void* stream);
+/* Advantage normalisation, two passes.  phase 0: stats[0] = global count and stats[1] =
+ * global sum must be set (all-reduced across ranks) -> mean, stats[3] = local sum sq dev.
+ * phase 1 (after all-reducing stats[3]): stats[4] = unbiased std. */
+int dxrl_pg_adv_finalize(int32_t device, int32_t phase, const float* adv, int64_t count, double* partial,
+                         double* stats, void* stream);
+
+typedef struct dxrl_pg_heads_args {
+    const float* mu;           /* f32 [M][32] actor head output            */
+    const float* values;       /* f32 [M] critic value                     */
+    const float* act;          /* f32 [M][16]                              */
+    const float* logp_old;     /* f32 [M]                                  */
+    const float* adv;          /* f32 [M] raw GAE advantages               */
+    const float* ret;          /* f32 [M] returns                          */
+    const double* stats;       /* normalisation stats (mean [2], std [4])  */
+    const float* params;       /* f32 master parameters (log_std)          */
+    int64_t num_samples;       /* M (this rank)                            */
+    double inv_total_samples;  /* 1 / (M summed over ranks)                */
+    double clip_eps, vf_coef, ent_coef;
+    void* dmu_rm;              /* bf16 [M][32]                             */
+    void* dmu_fm;              /* bf16 [32][M]                             */
+    void* dv_rm;               /* bf16 [M][32] (column 0)                  */
+    void* dv_fm;               /* bf16 [32][M] (row 0)                     */
+    float* dlogstd_partial;    /* f32 [ceil(M/256)][16]                    */
+    double* loss_partial;      /* f64 [ceil(M/256)][4]                     */
+    float* grads;              /* f32 master-layout gradients (log_std block written) */
+} dxrl_pg_heads_args;
+
+/* PPO-clip policy loss + value loss + entropy bonus: gradients at the heads. */
+int dxrl_pg_heads(int32_t device, const dxrl_pg_heads_args* args, void* stream);
+/* out[0] = sum(grads^2) (for global-norm clipping; all-reduce before Adam when sharded). */
+int dxrl_pg_grad_sumsq(int32_t device, const float* grads, int64_t n, double* partial, double* out, void* stream);
+int dxrl_pg_adam(int32_t device, float* params, const float* grads, float* m1, float* m2, int64_t n, double lr,
+                 double beta1, double beta2, double eps, int64_t step, const double* gnorm2, double max_norm,
+                 void* stream);
 
 #ifdef __cplusplus
 }

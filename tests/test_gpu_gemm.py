@@ -28,7 +28,7 @@ def gemm(N, A, Bt, *, bias=None, bias_stride=1, act=0, gate=None, out_f32=True, 
     partial = torch.empty(splits, M, Nn, dtype=torch.float32, device=dev) if splits > 1 else None
     p = N.ptr
     N.call("dxrl_gemm_bf16", dev.index, p(A), A.stride(0), p(Bt), Bt.stride(0), M, Nn, K, p(bias), bias_stride, act,
-           p(gate), 0 if gate is None else gate.stride(0), p(Cf), Nn, p(Crm), Nn, p(Cfm), M, splits, p(partial),
+           p(gate), 0 if gate is None else gate.stride(0), p(Cf), Nn, p(Crm), Nn, p(Cfm), M, None, 0, splits, p(partial),
            N.stream_of(dev))
     torch.cuda.synchronize()
     return Cf, Crm, Cfm

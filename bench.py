@@ -2,16 +2,22 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--horizon 200]
 
-One bench "step" = one training iteration of the hot path over one batch:
-every env of the shard advances `horizon` env steps (select_action -> step ->
-reward -> learner update, auto-reset at episode end) -- the reference's
-run_episode + SimpleLearner loop (training/episode_utils.py:13-55) fused into
-one HIP launch.  Workload = BASELINE configs[1]: config_easy curriculum,
-dense reward, 4096 envs per GPU, synthetic (device Philox) randomness.
+One bench "step" = one training iteration of the hot path over one batch
+(BASELINE configs[1]: config_easy curriculum, dense reward, 4096 envs per
+GPU, MLP(256,256) learner, synthetic device-Philox randomness):
 
-Multi-GPU (torchrun, one rank per GPU): env shards are independent replicas
-(global env ids rank*N .. rank*N+N-1), no data-path collective; the timing
-uses a barrier + max-over-ranks.  value = all ranks' env steps / max time.
+  --learner pg (default): PGTrainer.iteration() -- every env advances
+      `horizon` env steps with the actor MLP fused into the step kernel, then
+      critic forward, GAE, advantage normalisation, PPO heads, backward GEMMs,
+      gradient all-reduce (RCCL, world > 1) and Adam.
+  --learner simple: the reference's run_episode + SimpleLearner loop
+      (training/episode_utils.py:13-55, policies/simple_learner.py) for
+      `horizon` steps per env, fused into one HIP launch.
+
+Multi-GPU (torchrun, one rank per GPU): env shards are independent (global env
+ids rank*N .. rank*N+N-1); the PG learner all-reduces one flat f32 gradient
+buffer per iteration; the timing uses a barrier + max-over-ranks.
+value = all ranks' env steps / max time (weak scaling).
 
 Also measured in-process (HIP events on the launch stream):
   * roofline: the standalone step kernel (dxrl_env_step, k_step) at a large N
@@ -44,6 +50,8 @@ def parse():
     p.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     p.add_argument("--horizon", type=int, default=200, help="env steps per bench step (rollout length)")
     p.add_argument("--curriculum", default="easy")
+    p.add_argument("--learner", choices=["pg", "simple"], default="pg",
+                   help="pg: MLP actor-critic policy-gradient iteration (default); simple: SimpleLearner rollout")
     p.add_argument("--roofline-envs", type=int, default=1 << 22)
     p.add_argument("--roofline-launches", type=int, default=30)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -78,6 +86,65 @@ def max_over_ranks(x, world, dev):
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+# Algorithmic FLOPs per env-step (unpadded 45->256->256->{15,1} shapes):
+FWD_ACTOR = 2 * (45 * 256 + 256 * 256 + 256 * 15)      # 161,792 (rollout policy, per env step)
+FWD_BOTH = FWD_ACTOR + 2 * (45 * 256 + 256 * 256 + 256)  # 316,416 (training forward, both nets)
+BWD_BOTH = FWD_BOTH + 2 * (256 * 256 + 256 * 15) + 2 * (256 * 256 + 256)  # weight + input grads
+PEAK_BF16_TFS = 2500.0  # dense bf16 MFMA peak (MI355X_MICROARCH.md)
+
+
+def pg_bench(args, world, rank, dev):
+    """One bench step = one PGTrainer.iteration(): rollout (T env steps of every env, actor
+    MLP fused) + critic forward + GAE + adv-norm + actor forward + heads + backward +
+    RCCL gradient all-reduce (world > 1) + Adam."""
+    import dexterous_rl_manipulation_amd as pkg
+    from dexterous_rl_manipulation_amd import envs, trainer
+    n = args.envs
+    env = envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.named(args.curriculum), reward_type="dense",
+                      seed=20240601, device=dev, global_env_offset=rank * n)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        pg = dist.group.WORLD
+    tr = trainer.PGTrainer(env, trainer.TrainerConfig(horizon=args.horizon, seed=7), process_group=pg,
+                           world_size=world)
+    env.reset(write_obs=False)
+    for _ in range(args.warmup):
+        tr.iteration()
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.iteration()
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    wall = time.perf_counter() - t0
+    wall = max_over_ranks(wall, world, dev)
+    # phase breakdown (one extra iteration, outside the timed region)
+    stream = torch.cuda.current_stream(dev)
+    names = ["rollout", "critic_forward", "advantages", "actor_forward", "heads", "backward", "optimizer_step"]
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
+    evs[0].record(stream)
+    for k, nm in enumerate(names):
+        getattr(tr, nm)()
+        evs[k + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    phases = {nm: round(evs[k].elapsed_time(evs[k + 1]), 4) for k, nm in enumerate(names)}
+    M = tr.M
+    gemm_ms = phases["critic_forward"] + phases["actor_forward"] + phases["backward"]
+    train_flops = M * (FWD_BOTH + BWD_BOTH)
+    mfma = {"bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_BF16_TFS,
+            "training_gemms_achieved": round(train_flops / (gemm_ms * 1e-3) / 1e12, 2),
+            "rollout_policy_achieved": round(M * FWD_ACTOR / (phases["rollout"] * 1e-3) / 1e12, 2),
+            "algorithmic_flop_per_env_step": {"rollout_actor_fwd": FWD_ACTOR, "train_fwd": FWD_BOTH,
+                                              "train_bwd": BWD_BOTH}}
+    mfma["frac"] = round(mfma["training_gemms_achieved"] / PEAK_BF16_TFS, 4)
+    stats = tr.episode_stats()
+    stats.update({k: round(v, 5) for k, v in tr.loss_stats().items()})
+    return wall, phases, mfma, stats
 
 
 def rollout_bench(args, world, rank, dev):
@@ -186,21 +253,34 @@ def main():
     args = parse()
     world, rank, local = dist_setup(args)
     dev = torch.device("cuda", local if world > 1 else 0)
-    wall, kernel_ms = rollout_bench(args, world, rank, dev)
     total_steps = args.envs * world * args.horizon * args.steps
+    extra = {}
+    if args.learner == "pg":
+        wall, phases, mfma, stats = pg_bench(args, world, rank, dev)
+        workload = (f"config_{args.curriculum}.json PG iteration: fused actor-MLP(256,256) rollout of "
+                    f"{args.horizon} env steps x {args.envs} envs + critic fwd + GAE + adv-norm + PPO heads + "
+                    f"backward + Adam")
+        dtype = "bf16 MFMA (f32 acc) + f32/f64 env"
+        par = f"dp{world} (env shards, RCCL all-reduce of f32 grads)" if world > 1 else "dp1"
+        extra = {"phases_ms": phases, "mfma": mfma, "train_stats": stats}
+    else:
+        wall, kernel_ms = rollout_bench(args, world, rank, dev)
+        workload = (f"config_{args.curriculum}.json fused rollout: run_episode x SimpleLearner, dense reward, "
+                    f"{args.horizon} env steps per bench step")
+        dtype = "f32+f64"
+        par = f"env-shard replicas x{world} (no collective)"
+        extra = {"rollout_kernel_ms": round(kernel_ms, 4)}
     value = total_steps / wall
     out = {
         "metric": "env-steps/sec @4096 envs/GPU, 1/2/4/8 MI355X; %HBM roofline step kernel",
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32+f64",
-        "data": "synthetic (device Philox4x32-10 reset draws and learner noise)",
-        "config": {"workload": f"config_{args.curriculum}.json fused rollout: run_episode x SimpleLearner, dense "
-                               f"reward, {args.horizon} env steps per bench step",
-                   "envs_per_gpu": args.envs, "global_envs": args.envs * world, "horizon": args.horizon,
-                   "parallelism": f"env-shard replicas x{world} (no collective)",
-                   "rollout_kernel_ms": round(kernel_ms, 4)},
+        "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+        "data": "synthetic (device Philox4x32-10 reset draws, policy / learner noise; random-init weights)",
+        "config": {"workload": workload, "learner": args.learner, "envs_per_gpu": args.envs,
+                   "global_envs": args.envs * world, "horizon": args.horizon, "parallelism": par},
     }
+    out.update(extra)
     if rank == 0 and not args.no_roofline:
         out["roofline"] = step_kernel_roofline(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -106,6 +106,7 @@ _SIGS = {
                                       C.POINTER(RolloutIO), _P]),
     "dxrl_gemm_bf16": (C.c_int, [_I32, _P, _I64, _P, _I64, _I64, _I32, _I32, _P, _I64, _I32, _P, _I64, _P, _I64,
                                  _P, _I64, _P, _I64, _P, _I64, _I32, _P, _P]),
+    "dxrl_wgrad_bf16": (C.c_int, [_I32, _P, _I64, _I32, _P, _I64, _I32, _I64, _I32, _P, _P, _P]),
     "dxrl_pg_sizes": (C.c_int, [C.POINTER(_I64), C.POINTER(_I64)]),
     "dxrl_pg_pack_weights": (C.c_int, [_I32, _P, _P, _P]),
     "dxrl_pg_rollout": (C.c_int, [_P, _P, _P, C.POINTER(PgRolloutArgs), _P]),

@@ -32,5 +32,8 @@ struct GemmArgs {
 // Launch C = epi(A . Bt^T); splits > 1 -> split-K partial slabs reduced into
 // reduce_out (f32 [M][N], += when accumulate).
 int launch_gemm(const GemmArgs& g, int splits, float* reduce_out, int accumulate, hipStream_t st);
+// out[O][I] = sum_m Y[m][o] X[m][i] (row-major operands, split-K over m).
+int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, int I, int64_t M, int splits,
+                 float* partial, float* out, hipStream_t st);
 
 }  // namespace dxrl

@@ -1,12 +1,16 @@
-// dxrl_gemm.hip -- bf16 MFMA GEMM with fused epilogues for the actor-critic.
+// dxrl_gemm.hip -- bf16 MFMA GEMMs with fused epilogues for the actor-critic.
 //
-// C[M][N] = epi( A[M][K] . Bt[N][K]^T ), f32 accumulate.  Used for every
-// dense obs x W contraction of the policy-gradient learner (forward, input
-// gradients, weight gradients with split-K over samples).  Workgroup = 4
-// waves (2x2), wave tile 64x64 = 2x2 MFMA 32x32x16 tiles, K step 32.
-// Operand fragments are loaded straight from global memory (16 B / lane);
-// the weight operand is L2-resident (<= 150 KB per matrix), activations
-// stream once per column block.
+// k_gemm_bf16 : C[M][N] = epi(A[M][K] . Bt[N][K]^T)  (forward layers, input grads)
+// k_wgrad_bf16: C[O][I] = sum_m Y[m][O] X[m][I]       (weight grads, split-K over samples)
+//
+// Both stage 128x64 / 64x128 bf16 tiles through LDS with coalesced 16-byte
+// global loads (8 or 16 lanes per contiguous row segment), double-buffered
+// through registers: the next tile's global loads are issued before the
+// current tile's MFMAs.  Workgroup = 4 waves (2x2), wave tile 64x64 =
+// 2x2 v_mfma_f32_32x32x16_bf16.  The weight-gradient kernel reads both
+// row-major operands k-major straight out of LDS with ds_read_b64_tr_b16
+// (gfx950 transpose read, cdna_hip_programming.md T10), so no feature-major
+// copy of any activation is ever written.
 #include "dxrl_internal.h"
 #include "dxrl_gemm.h"
 
@@ -14,15 +18,33 @@ using namespace dxrl;
 
 namespace dxrl {
 
-constexpr int kWaveTile = 64, kBlockM = 128, kBlockN = 128;
+typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef __attribute__((address_space(3))) bf16 lds_bf16;
 
+constexpr int kBM = 128, kBN = 128, kBK = 64;
+constexpr int kAPitch = kBK + 8;  // 144-B rows: conflict-free ds_read_b128 fragment reads
+
+__device__ __forceinline__ bf16x8 zero8() {
+    bf16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = (bf16)0.0f;
+    return z;
+}
+
+// ------------------------------------------------------------------ C = A . Bt^T
 __global__ __launch_bounds__(256) void k_gemm_bf16(GemmArgs g) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ __attribute__((aligned(16))) bf16 As[kBM * kAPitch];
+    __shared__ __attribute__((aligned(16))) bf16 Bs[kBN * kAPitch];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int64_t m0 = (int64_t)blockIdx.x * kBlockM + (wave & 1) * kWaveTile;
-    const int n0 = blockIdx.y * kBlockN + (wave >> 1) * kWaveTile;
+    const int wm = (wave & 1) * 64, wn = (wave >> 1) * 64;
+    const int64_t m0 = (int64_t)blockIdx.x * kBM;
+    const int n0 = blockIdx.y * kBN;
     const int64_t kb = (int64_t)blockIdx.z * g.k_chunk;
     const int64_t ke = min((int64_t)g.K, kb + g.k_chunk);
+    const bool wave_live = (n0 + wn) < g.N;
+
     f32x16 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -31,36 +53,62 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(GemmArgs g) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.0f;
 
-    if (n0 < g.N && m0 < g.M) {
-        for (int64_t k = kb; k < ke; k += 32) {
-            bf16x8 a[2][2], b[2][2];
+    // each thread moves 4 A chunks and 4 B chunks of 16 B per tile: chunk c -> row c>>3, col 8*(c&7)
+    bf16x8 ra[4], rb[4];
+    auto fetch = [&](int64_t k0) {
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int kk = (int)(k + 16 * s + 8 * h);
+        for (int q = 0; q < 4; ++q) {
+            const int c = tid + 256 * q, row = c >> 3, col = 8 * (c & 7);
+            const int64_t k = k0 + col;
+            const int64_t m = m0 + row;
+            ra[q] = (m < g.M && k < ke) ? *reinterpret_cast<const bf16x8*>(g.A + m * g.lda + k) : zero8();
+            const int n = n0 + row;
+            rb[q] = (n < g.N && k < ke) ? *reinterpret_cast<const bf16x8*>(g.Bt + (int64_t)n * g.ldb + k) : zero8();
+        }
+    };
+    auto stash = [&]() {
 #pragma unroll
-                for (int i = 0; i < 2; ++i) a[s][i] = load_frag(g.A, g.lda, m0 + 32 * i + r, g.M, kk);
+        for (int q = 0; q < 4; ++q) {
+            const int c = tid + 256 * q, row = c >> 3, col = 8 * (c & 7);
+            *reinterpret_cast<bf16x8*>(As + row * kAPitch + col) = ra[q];
+            *reinterpret_cast<bf16x8*>(Bs + row * kAPitch + col) = rb[q];
+        }
+    };
+    if (kb < ke) fetch(kb);
+    for (int64_t k0 = kb; k0 < ke; k0 += kBK) {
+        __syncthreads();  // previous tile's fragment reads are done
+        stash();
+        __syncthreads();
+        if (k0 + kBK < ke) fetch(k0 + kBK);  // overlaps with the MFMAs below
+        if (wave_live) {
 #pragma unroll
-                for (int j = 0; j < 2; ++j) b[s][j] = load_frag(g.Bt, g.ldb, n0 + 32 * j + r, g.N, kk);
-            }
+            for (int kk = 0; kk < kBK; kk += 16) {
+                bf16x8 a[2], b[2];
 #pragma unroll
-            for (int s = 0; s < 2; ++s)
+                for (int i = 0; i < 2; ++i)
+                    a[i] = *reinterpret_cast<const bf16x8*>(As + (wm + 32 * i + r) * kAPitch + kk + 8 * h);
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    b[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn + 32 * j + r) * kAPitch + kk + 8 * h);
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[s][i], b[s][j], acc[i][j]);
+                    for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+            }
         }
     }
+    if (!wave_live) return;
     // ---- epilogue
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-        const int n = n0 + 32 * j + r;
+        const int n = n0 + wn + 32 * j + r;
         if (n >= g.N) continue;
         const float bias = g.bias ? g.bias[(int64_t)n * g.bias_stride] : 0.0f;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int64_t m = m0 + 32 * i + acc_row(q, lane);
+                const int64_t m = m0 + wm + 32 * i + acc_row(q, lane);
                 if (m >= g.M) continue;
                 float v = acc[i][j][q];
                 if (g.partial) {
@@ -83,6 +131,113 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(GemmArgs g) {
     }
 }
 
+// ------------------------------------------------------------------ C[O][I] = Y^T X
+// LDS images are [64 samples][128 features] bf16 with 320-B rows: the
+// transposed reads (rows 16kk + 8(g>>1) + q, columns 16(g&1) + 4p of a
+// 16-lane group g) then touch all 64 banks once per 32-lane half.
+constexpr int kWO = 128, kWI = 128, kWK = 64, kWPitch = 128 + 32;
+
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int col0, int kk, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int row = kk + 8 * (g >> 1) + q;
+    const int col = col0 + 16 * (g & 1) + 4 * p;
+    lds_bf16* base = (lds_bf16*)(tile);  // generic -> LDS address space (the tile is __shared__)
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + row * kWPitch + col));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + (row + 4) * kWPitch + col));
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = lo[j];
+        v[4 + j] = hi[j];
+    }
+    return v;
+}
+
+struct WgradArgs {
+    const bf16* Y;  // [M][ldy], O used columns
+    int64_t ldy;
+    const bf16* X;  // [M][ldx], I used columns
+    int64_t ldx;
+    int O, I;
+    int64_t M, m_chunk;
+    float* out;      // [O][I] f32 (splits == 1)
+    float* partial;  // [splits][O][I] (splits > 1)
+};
+
+__global__ __launch_bounds__(256) void k_wgrad_bf16(WgradArgs w) {
+    __shared__ __attribute__((aligned(16))) bf16 Ys[kWK * kWPitch];
+    __shared__ __attribute__((aligned(16))) bf16 Xs[kWK * kWPitch];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wo = (wave & 1) * 64, wi = (wave >> 1) * 64;
+    const int o0 = blockIdx.x * kWO, i0 = blockIdx.y * kWI;
+    const int64_t mb = (int64_t)blockIdx.z * w.m_chunk;
+    const int64_t me = min(w.M, mb + w.m_chunk);
+    const bool wave_live = (o0 + wo) < w.O && (i0 + wi) < w.I;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.0f;
+    // tile = 64 rows x 16 chunks of 16 B: chunk c -> row c >> 4, col 8 (c & 15)
+    bf16x8 ry[4], rx[4];
+    auto fetch = [&](int64_t m0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = tid + 256 * q, row = c >> 4, col = 8 * (c & 15);
+            const int64_t m = m0 + row;
+            const bool mv = m < me;
+            ry[q] = (mv && o0 + col < w.O) ? *reinterpret_cast<const bf16x8*>(w.Y + m * w.ldy + o0 + col) : zero8();
+            rx[q] = (mv && i0 + col < w.I) ? *reinterpret_cast<const bf16x8*>(w.X + m * w.ldx + i0 + col) : zero8();
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = tid + 256 * q, row = c >> 4, col = 8 * (c & 15);
+            *reinterpret_cast<bf16x8*>(Ys + row * kWPitch + col) = ry[q];
+            *reinterpret_cast<bf16x8*>(Xs + row * kWPitch + col) = rx[q];
+        }
+    };
+    if (mb < me) fetch(mb);
+    for (int64_t m0 = mb; m0 < me; m0 += kWK) {
+        __syncthreads();
+        stash();
+        __syncthreads();
+        if (m0 + kWK < me) fetch(m0 + kWK);
+        // every lane of the wave issues the transposed reads (EXEC must be all ones)
+#pragma unroll
+        for (int kk = 0; kk < kWK; kk += 16) {
+            bf16x8 a[2], b[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) a[i] = tr_frag(Ys, wo + 32 * i, kk, lane);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b[j] = tr_frag(Xs, wi + 32 * j, kk, lane);
+            if (wave_live) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+            }
+        }
+    }
+    if (!wave_live) return;
+    float* dst = w.partial ? w.partial + (int64_t)blockIdx.z * w.O * w.I : w.out;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int i = i0 + wi + 32 * j + (lane & 31);
+        if (i >= w.I) continue;
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int o = o0 + wo + 32 * ii + acc_row(q, lane);
+                if (o < w.O) dst[(int64_t)o * w.I + i] = acc[ii][j][q];
+            }
+    }
+}
+
 // out[i] (+)= sum_z partial[z][i], fixed order (deterministic)
 __global__ void k_splitk_reduce(const float* __restrict__ partial, int64_t slab, int z, float* __restrict__ out,
                                 int accumulate) {
@@ -101,18 +256,43 @@ int launch_gemm(const GemmArgs& g0, int splits, float* reduce_out, int accumulat
                  "gemm: operands must be 16-byte aligned");
     if (splits < 1) splits = 1;
     int64_t chunk = (g.K + splits - 1) / splits;
-    chunk = (chunk + 31) / 32 * 32;
+    chunk = (chunk + kBK - 1) / kBK * kBK;
     splits = (int)((g.K + chunk - 1) / chunk);
     g.k_chunk = chunk;
     if (splits > 1) DXRL_REQUIRE(g.partial && reduce_out, "gemm: split-K needs a partial slab and an output");
-    const dim3 grid((unsigned)((g.M + kBlockM - 1) / kBlockM), (unsigned)((g.N + kBlockN - 1) / kBlockN),
-                    (unsigned)splits);
+    if (splits == 1) g.partial = nullptr;
+    const dim3 grid((unsigned)((g.M + kBM - 1) / kBM), (unsigned)((g.N + kBN - 1) / kBN), (unsigned)splits);
     hipLaunchKernelGGL(k_gemm_bf16, grid, dim3(256), 0, st, g);
     if (int rc = launch_check("k_gemm_bf16")) return rc;
     if (g.partial) {
         const int64_t slab = g.M * (int64_t)g.N;
         hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, st, g.partial, slab,
                            splits, reduce_out, accumulate);
+        if (int rc = launch_check("k_splitk_reduce")) return rc;
+    }
+    return DXRL_OK;
+}
+
+int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, int I, int64_t M, int splits,
+                 float* partial, float* out, hipStream_t st) {
+    DXRL_REQUIRE(Y && X && out && O > 0 && I > 0 && M > 0, "wgrad: bad arguments");
+    DXRL_REQUIRE(ldy % 8 == 0 && ldx % 8 == 0 && O % 8 == 0 && I % 8 == 0,
+                 "wgrad: leading dims and feature counts must be multiples of 8");
+    DXRL_REQUIRE((reinterpret_cast<uintptr_t>(Y) & 15) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0,
+                 "wgrad: operands must be 16-byte aligned");
+    if (splits < 1) splits = 1;
+    int64_t chunk = (M + splits - 1) / splits;
+    chunk = (chunk + kWK - 1) / kWK * kWK;
+    splits = (int)((M + chunk - 1) / chunk);
+    DXRL_REQUIRE(splits == 1 || partial, "wgrad: split-K needs a partial slab");
+    WgradArgs w{Y, ldy, X, ldx, O, I, M, chunk, out, splits > 1 ? partial : nullptr};
+    const dim3 grid((unsigned)((O + kWO - 1) / kWO), (unsigned)((I + kWI - 1) / kWI), (unsigned)splits);
+    hipLaunchKernelGGL(k_wgrad_bf16, grid, dim3(256), 0, st, w);
+    if (int rc = launch_check("k_wgrad_bf16")) return rc;
+    if (splits > 1) {
+        const int64_t slab = (int64_t)O * I;
+        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, st, partial, slab,
+                           splits, out, 0);
         if (int rc = launch_check("k_splitk_reduce")) return rc;
     }
     return DXRL_OK;
@@ -132,6 +312,13 @@ int dxrl_gemm_bf16(int32_t device, const void* A, int64_t lda, const void* Bt, i
                act, static_cast<const bf16*>(gate), ldg, Cf, ldcf, static_cast<bf16*>(Crm), ldc,
                static_cast<bf16*>(Cfm), ldfm, splits > 1 ? partial : nullptr, Cffm, ldffm};
     return launch_gemm(g, splits, splits > 1 ? Cf : nullptr, 0, as_stream(stream));
+}
+
+int dxrl_wgrad_bf16(int32_t device, const void* Y, int64_t ldy, int32_t O, const void* X, int64_t ldx, int32_t I,
+                    int64_t M, int32_t splits, float* partial, float* out, void* stream) {
+    DeviceGuard dg(device);
+    return launch_wgrad(static_cast<const bf16*>(Y), ldy, O, static_cast<const bf16*>(X), ldx, I, M, splits, partial,
+                        out, as_stream(stream));
 }
 
 }  // extern "C"

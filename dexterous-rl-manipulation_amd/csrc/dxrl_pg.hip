@@ -393,12 +393,12 @@ __global__ __launch_bounds__(256) void k_ppo_heads(HeadArgs h) {
             const float dmu = g * d * iv;              // dlogp/dmu = (a - mu) / sigma^2
             dls[k] = g * (d * d * iv - 1.0f);          // dlogp/dlogstd = (a-mu)^2/sigma^2 - 1
             h.dmu_rm[m * kOut + k] = to_bf16(dmu);
-            h.dmu_fm[(int64_t)k * h.M + m] = to_bf16(dmu);
+            if (h.dmu_fm) h.dmu_fm[(int64_t)k * h.M + m] = to_bf16(dmu);
         }
         const float v = h.V[m];
         const float dv = 2.0f * h.vf_coef * (v - h.ret[m]) * sc;
         h.dv_rm[m * kOut] = to_bf16(dv);
-        h.dv_fm[m] = to_bf16(dv);
+        if (h.dv_fm) h.dv_fm[m] = to_bf16(dv);
         lp_loss = -(double)fminf(s1, s2);
         lv = (double)(v - h.ret[m]) * (double)(v - h.ret[m]);
         clipped = fabsf(ratio - 1.0f) > h.clip_eps ? 1.0 : 0.0;

@@ -98,8 +98,6 @@ class PGTrainer:
         self._init_params()
         # tape
         self.obs_rm = z((T + 1) * n, IN, dt=bf)
-        self.obs_fm = z(IN, M, dt=bf)
-        self.obs_fm[OBS_IN].fill_(1.0)
         self.act = z(M, ACT_PAD)
         self.logp, self.rew = z(M), z(M)
         self.done = z(M, dt=torch.uint8)
@@ -108,23 +106,23 @@ class PGTrainer:
         self.ep_sum_ret = torch.zeros(n, dtype=torch.float64, device=d)
         self.ep_sum_len = z(n, dt=torch.int32)
         self.ep_succ = z(n, dt=torch.int32)
-        # activations (row-major A operands / gates, feature-major weight-grad operands with a ones row)
-        self.H1a, self.H2a = z(M, H, dt=bf), z(M, H, dt=bf)
-        self.H1c, self.H2c = z((T + 1) * n, H, dt=bf), z((T + 1) * n, H, dt=bf)
-        self.H1a_fm, self.H2a_fm, self.H1c_fm, self.H2c_fm = (z(HX, M, dt=bf) for _ in range(4))
-        for t in (self.H1a_fm, self.H2a_fm, self.H1c_fm, self.H2c_fm):
-            t[H].fill_(1.0)
+        # hidden activations, row-major [rows][288]: columns 0..255 = tanh units, column 256 = 1
+        # (the next layer reads K = 256; the weight-gradient GEMM reads I = 288 and gets the bias
+        # gradient as column 256)
+        self.H1a, self.H2a = z(M, HX, dt=bf), z(M, HX, dt=bf)
+        self.H1c, self.H2c = z((T + 1) * n, HX, dt=bf), z((T + 1) * n, HX, dt=bf)
+        for t in (self.H1a, self.H2a, self.H1c, self.H2c):
+            t[:, H].fill_(1.0)
         self.mu = z(M, OUT)
         self.V = z(OUT, (T + 1) * n)
         self.adv, self.ret = z(M), z(M)
         self.stats = torch.zeros(8, dtype=torch.float64, device=d)
         nb = max(1024, (M + 255) // 256, (n + 255) // 256)
         self.partial = torch.zeros(nb, dtype=torch.float64, device=d)
-        self.dmu_rm, self.dmu_fm = z(M, OUT, dt=bf), z(OUT, M, dt=bf)
-        self.dv_rm, self.dv_fm = z(M, OUT, dt=bf), z(OUT, M, dt=bf)
+        self.dmu_rm, self.dv_rm = z(M, OUT, dt=bf), z(M, OUT, dt=bf)
         self.dls_partial = z((M + 255) // 256, ACT_PAD)
         self.loss_partial = torch.zeros((M + 255) // 256, 4, dtype=torch.float64, device=d)
-        self.dH2_rm, self.dH2_fm, self.dH1_fm = z(M, H, dt=bf), z(H, M, dt=bf), z(H, M, dt=bf)
+        self.dH2, self.dH1 = z(M, H, dt=bf), z(M, H, dt=bf)
         self.splits = max(1, min(cfg.splitk_target_blocks // 6, M // 4096))
         self.kpartial = z(self.splits, H, HX)
         self.gnorm2 = torch.zeros(1, dtype=torch.float64, device=d)
@@ -165,10 +163,11 @@ class PGTrainer:
         N.call("dxrl_gemm_bf16", self.dev.index, p(A), lda, p(Bt), ldb, M, Nn, K, p(bias), bias_stride, act, p(gate),
                ldg, p(Cf), ldcf, p(Crm), ldc, p(Cfm), ldfm, p(Cffm), ldffm, splits, p(partial), self._s())
 
-    def _wgrad(self, A_fm, Bt_fm, rows, cols, dst):
-        """dst[rows][cols] = A_fm[rows][M] . Bt_fm[cols][M]^T (split-K over samples)."""
-        self._gemm(A_fm, self.M, Bt_fm, self.M, rows, cols, self.M, Cf=dst, ldcf=cols, splits=self.splits,
-                   partial=self.kpartial)
+    def _wgrad(self, Y, ldy, O, X, ldx, I, dst):
+        """dst[O][I] = sum_m Y[m][:O] X[m][:I] (row-major operands, split-K over samples)."""
+        p = N.ptr
+        N.call("dxrl_wgrad_bf16", self.dev.index, p(Y), ldy, O, p(X), ldx, I, self.M, self.splits,
+               p(self.kpartial), p(dst), self._s())
 
     def rollout(self):
         a = N.PgRolloutArgs()
@@ -177,35 +176,26 @@ class PGTrainer:
         a.iteration = self.iteration_index
         a.obs_noise_std, a.dyn_noise_std = self.cfg.obs_noise_std, self.cfg.dyn_noise_std
         p = N.ptr
-        a.obs_rm, a.obs_fm, a.act, a.logp, a.rew, a.done = (p(self.obs_rm), p(self.obs_fm), p(self.act),
-                                                            p(self.logp), p(self.rew), p(self.done))
+        a.obs_rm, a.obs_fm, a.act, a.logp, a.rew, a.done = (p(self.obs_rm), None, p(self.act), p(self.logp),
+                                                            p(self.rew), p(self.done))
         a.ep_return, a.ep_count, a.ep_sum_return = p(self.ep_ret), p(self.ep_count), p(self.ep_sum_ret)
         a.ep_sum_length, a.ep_successes = p(self.ep_sum_len), p(self.ep_succ)
         N.call("dxrl_pg_rollout", self.env.handle, p(self.packed), p(self.params), C.byref(a), self._s())
 
+    def _mlp_forward(self, net, rows, H1, H2, head_f32=None, head_fm=None, ld_head_fm=0):
+        P = self.params
+        self._gemm(self.obs_rm, IN, self._bf(f"W1{net}"), IN, rows, H, IN, act=1, Crm=H1, ldc=HX)  # bias = col 45
+        self._gemm(H1, HX, self._bf(f"W2{net}"), HX, rows, H, H, bias=P[OFF[f"W2{net}"] + H:], bias_stride=HX, act=1,
+                   Crm=H2, ldc=HX)
+        self._gemm(H2, HX, self._bf(f"W3{net}"), HX, rows, OUT, H, bias=P[OFF[f"W3{net}"] + H:], bias_stride=HX,
+                   Cf=head_f32, ldcf=OUT, Cffm=head_fm, ldffm=ld_head_fm)
+
     def critic_forward(self):
-        M, n, P = self.M, self.n, self.params
-        rows = M + n
-        # L1 (bias = column 45 of W1 against the constant-1 input): rows [0, M) also feature-major
-        self._gemm(self.obs_rm, IN, self._bf("W1c"), IN, M, H, IN, act=1, Crm=self.H1c, ldc=H, Cfm=self.H1c_fm,
-                   ldfm=M)
-        self._gemm(self.obs_rm[M:], IN, self._bf("W1c"), IN, n, H, IN, act=1, Crm=self.H1c[M:], ldc=H)
-        b2, b3 = P[OFF["W2c"] + H:], P[OFF["W3c"] + H:]
-        self._gemm(self.H1c, H, self._bf("W2c"), HX, M, H, H, bias=b2, bias_stride=HX, act=1, Crm=self.H2c,
-                   ldc=H, Cfm=self.H2c_fm, ldfm=M)
-        self._gemm(self.H1c[M:], H, self._bf("W2c"), HX, n, H, H, bias=b2, bias_stride=HX, act=1, Crm=self.H2c[M:],
-                   ldc=H)
-        self._gemm(self.H2c, H, self._bf("W3c"), HX, rows, OUT, H, bias=b3, bias_stride=HX, Cffm=self.V,
-                   ldffm=rows)
+        rows = self.M + self.n  # T + 1 observation blocks (bootstrap values)
+        self._mlp_forward("c", rows, self.H1c, self.H2c, head_fm=self.V, ld_head_fm=rows)
 
     def actor_forward(self):
-        M, P = self.M, self.params
-        self._gemm(self.obs_rm, IN, self._bf("W1a"), IN, M, H, IN, act=1, Crm=self.H1a, ldc=H, Cfm=self.H1a_fm,
-                   ldfm=M)
-        self._gemm(self.H1a, H, self._bf("W2a"), HX, M, H, H, bias=P[OFF["W2a"] + H:], bias_stride=HX, act=1,
-                   Crm=self.H2a, ldc=H, Cfm=self.H2a_fm, ldfm=M)
-        self._gemm(self.H2a, H, self._bf("W3a"), HX, M, OUT, H, bias=P[OFF["W3a"] + H:], bias_stride=HX, Cf=self.mu,
-                   ldcf=OUT)
+        self._mlp_forward("a", self.M, self.H1a, self.H2a, head_f32=self.mu)
 
     def _allreduce(self, t):
         if self.world > 1:
@@ -232,21 +222,18 @@ class PGTrainer:
         h.num_samples = self.M
         h.inv_total_samples = 1.0 / (self.M * self.world)
         h.clip_eps, h.vf_coef, h.ent_coef = c.clip_eps, c.vf_coef, c.ent_coef / self.world
-        h.dmu_rm, h.dmu_fm, h.dv_rm, h.dv_fm = p(self.dmu_rm), p(self.dmu_fm), p(self.dv_rm), p(self.dv_fm)
+        h.dmu_rm, h.dmu_fm, h.dv_rm, h.dv_fm = p(self.dmu_rm), None, p(self.dv_rm), None
         h.dlogstd_partial, h.loss_partial, h.grads = p(self.dls_partial), p(self.loss_partial), p(self.grads)
         N.call("dxrl_pg_heads", self.dev.index, C.byref(h), self._s())
 
     def backward(self):
         M, G = self.M, self.grads
-        for net, dY_rm, dY_fm, H1, H2, H1fm, H2fm in (
-                ("a", self.dmu_rm, self.dmu_fm, self.H1a, self.H2a, self.H1a_fm, self.H2a_fm),
-                ("c", self.dv_rm, self.dv_fm, self.H1c, self.H2c, self.H1c_fm, self.H2c_fm)):
-            self._wgrad(dY_fm, H2fm, OUT, HX, self.block(f"W3{net}", G))
-            self._gemm(dY_rm, OUT, self._bf(f"W3{net}T"), OUT, M, H, OUT, gate=H2, ldg=H, Crm=self.dH2_rm, ldc=H,
-                       Cfm=self.dH2_fm, ldfm=M)
-            self._wgrad(self.dH2_fm, H1fm, H, HX, self.block(f"W2{net}", G))
-            self._gemm(self.dH2_rm, H, self._bf(f"W2{net}T"), H, M, H, H, gate=H1, ldg=H, Cfm=self.dH1_fm, ldfm=M)
-            self._wgrad(self.dH1_fm, self.obs_fm, H, IN, self.block(f"W1{net}", G))
+        for net, dY, H1, H2 in (("a", self.dmu_rm, self.H1a, self.H2a), ("c", self.dv_rm, self.H1c, self.H2c)):
+            self._wgrad(dY, OUT, OUT, H2, HX, HX, self.block(f"W3{net}", G))
+            self._gemm(dY, OUT, self._bf(f"W3{net}T"), OUT, M, H, OUT, gate=H2, ldg=HX, Crm=self.dH2, ldc=H)
+            self._wgrad(self.dH2, H, H, H1, HX, HX, self.block(f"W2{net}", G))
+            self._gemm(self.dH2, H, self._bf(f"W2{net}T"), H, M, H, H, gate=H1, ldg=HX, Crm=self.dH1, ldc=H)
+            self._wgrad(self.dH1, H, H, self.obs_rm, IN, IN, self.block(f"W1{net}", G))
 
     def optimizer_step(self):
         c = self.cfg

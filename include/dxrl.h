@@ -203,6 +203,11 @@ int dxrl_gemm_bf16(int32_t device, const void* A, int64_t lda, const void* Bt, i
                    int32_t K, const float* bias, int64_t bias_stride, int32_t act, const void* gate, int64_t ldg,
                    float* Cf, int64_t ldcf, void* Crm, int64_t ldc, void* Cfm, int64_t ldfm, float* Cffm,
                    int64_t ldffm, int32_t splits, float* partial, void* stream);
+/* Weight gradient out[O][I] = sum_m Y[m][o] X[m][i] from row-major bf16 operands
+ * (k-major MFMA operands via ds_read_b64_tr_b16); split-K over m into `partial`
+ * (f32 [splits][O][I]) reduced in fixed order (deterministic).  O, I, ldy, ldx % 8 == 0. */
+int dxrl_wgrad_bf16(int32_t device, const void* Y, int64_t ldy, int32_t O, const void* X, int64_t ldx, int32_t I,
+                    int64_t M, int32_t splits, float* partial, float* out, void* stream);
 
 /* ------------------------------------------------------------------------
  * Policy-gradient learner (NEW capability: the reference has no network,

@@ -80,3 +80,39 @@ def test_gemm_split_k_weight_gradient_shape(N):
     torch.testing.assert_close(Cf, ref, rtol=1e-4, atol=2e-3)
     Cf2, _, _ = gemm(N, dYfm, Xfm, splits=13)
     assert torch.equal(Cf, Cf2)  # deterministic
+
+
+def wgrad(N, Y, O, X, I, splits=1):
+    M = Y.shape[0]
+    dev = Y.device
+    out = torch.full((O, I), float("nan"), dtype=torch.float32, device=dev)
+    partial = torch.empty(max(splits, 1), O, I, dtype=torch.float32, device=dev)
+    p = N.ptr
+    N.call("dxrl_wgrad_bf16", dev.index, p(Y), Y.stride(0), O, p(X), X.stride(0), I, M, splits, p(partial), p(out),
+           N.stream_of(dev))
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("M,O,ldy,I,ldx,splits", [(64, 128, 128, 128, 128, 1), (1000, 256, 256, 288, 288, 1),
+                                                  (4096, 32, 32, 288, 288, 7), (3232, 256, 256, 64, 64, 5),
+                                                  (50016, 256, 256, 288, 288, 33)])
+def test_wgrad_transposed_lds_reads(N, M, O, ldy, I, ldx, splits):
+    """out[o][i] = sum_m Y[m][o] X[m][i] from row-major operands (ds_read_b64_tr_b16 path)."""
+    g = torch.Generator(device="cuda").manual_seed(M + O + I)
+    Y = (0.1 * torch.randn(M, ldy, device="cuda", generator=g)).to(torch.bfloat16)
+    X = torch.randn(M, ldx, device="cuda", generator=g).to(torch.bfloat16)
+    out = wgrad(N, Y, O, X, I, splits)
+    ref = Y[:, :O].float().T @ X[:, :I].float()
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3 * (M / 1000) ** 0.5)
+
+
+def test_wgrad_exact_integer_asymmetric(N):
+    """Exact small integers: any transpose / k-order slip shows as a hard mismatch."""
+    M, O, I = 128, 32, 64
+    Y = (torch.arange(M * O, device="cuda").reshape(M, O) % 7 - 3).to(torch.bfloat16)
+    X = (torch.arange(M * I, device="cuda").reshape(M, I) % 5 - 2).float().mul(torch.arange(I, device="cuda") % 3 + 1)
+    X = X.to(torch.bfloat16)
+    out = wgrad(N, Y, O, X, I)
+    ref = Y.float().T @ X.float()
+    assert torch.equal(out, ref)

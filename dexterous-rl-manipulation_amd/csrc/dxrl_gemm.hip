@@ -131,6 +131,126 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(GemmArgs g) {
     }
 }
 
+// ------------------------------------------------------------------ panel GEMM
+// Tall-skinny layers of the learner (M ~ 1e6 samples, N <= 256, K <= 256):
+// a workgroup owns a 64-row panel and ALL output columns, so each activation
+// row is read from HBM exactly once.  The whole A panel (and the tanh' gate
+// panel) is fetched with every 16-byte load in flight at once, then each wave
+// computes 64 rows x 64 columns with B fragments from L2; the bf16 result is
+// staged in LDS and leaves as full 16-byte-per-lane row segments.
+constexpr int kPM = 64, kPK = 256, kPPitch = kPK + 8;  // 528-B LDS rows
+
+__global__ __launch_bounds__(256) void k_gemm_panel(GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) bf16 Ap[kPM * kPPitch];  // A panel, then the bf16 output stage
+    __shared__ __attribute__((aligned(16))) bf16 Gp[kPM * kPPitch];  // gate panel (tanh')
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t m0 = (int64_t)blockIdx.x * kPM;
+    const int K = g.K, Nn = g.N;
+    const int kc = K >> 3;  // 16-byte chunks per row
+    // ---- panel loads: every chunk of the A (and gate) panel in flight together
+    {
+        bf16x8 ta[8], tg[8];
+        const int na = kPM * kc, ng = g.gate ? kPM * (Nn >> 3) : 0, gc = Nn >> 3;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int c = tid + 256 * q;
+            if (c < na) {
+                const int64_t m = m0 + c / kc;
+                ta[q] = m < g.M ? *reinterpret_cast<const bf16x8*>(g.A + m * g.lda + 8 * (c % kc)) : zero8();
+            }
+            if (c < ng) {
+                const int64_t m = m0 + c / gc;
+                tg[q] = m < g.M ? *reinterpret_cast<const bf16x8*>(g.gate + m * g.ldg + 8 * (c % gc)) : zero8();
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int c = tid + 256 * q;
+            if (c < na) *reinterpret_cast<bf16x8*>(Ap + (c / kc) * kPPitch + 8 * (c % kc)) = ta[q];
+            if (c < ng) *reinterpret_cast<bf16x8*>(Gp + (c / gc) * kPPitch + 8 * (c % gc)) = tg[q];
+        }
+    }
+    __syncthreads();
+    const int wn = 64 * wave;
+    const bool live = wn < Nn;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.0f;
+    if (live) {
+        const bf16* B0 = g.Bt + (int64_t)(wn + r) * g.ldb + 8 * h;
+        const bf16* B1 = g.Bt + (int64_t)(wn + 32 + r) * g.ldb + 8 * h;
+        const bool b1ok = wn + 32 + r < Nn, b0ok = wn + r < Nn;
+        // B fragments (weights, L2-resident): issue four k-steps of loads ahead of their MFMAs
+        for (int k0 = 0; k0 < K; k0 += 64) {
+            bf16x8 b0[4], b1[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = k0 + 16 * s;
+                b0[s] = (b0ok && k < K) ? *reinterpret_cast<const bf16x8*>(B0 + k) : zero8();
+                b1[s] = (b1ok && k < K) ? *reinterpret_cast<const bf16x8*>(B1 + k) : zero8();
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = k0 + 16 * s;
+                if (k >= K) break;
+                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Ap + r * kPPitch + k + 8 * h);
+                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Ap + (32 + r) * kPPitch + k + 8 * h);
+                acc[0][0] = mfma32(a0, b0[s], acc[0][0]);
+                acc[0][1] = mfma32(a0, b1[s], acc[0][1]);
+                acc[1][0] = mfma32(a1, b0[s], acc[1][0]);
+                acc[1][1] = mfma32(a1, b1[s], acc[1][1]);
+            }
+        }
+    }
+    __syncthreads();  // A panel reads done: Ap becomes the output stage
+    if (live) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = wn + 32 * j + r;
+            const bool nv = n < Nn;
+            const float bias = (g.bias && nv) ? g.bias[(int64_t)n * g.bias_stride] : 0.0f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int row = 32 * i + acc_row(q, lane);
+                    const int64_t m = m0 + row;
+                    float v = acc[i][j][q] + bias;
+                    if (g.act == 1) v = tanh_f(v);
+                    if (g.gate) {
+                        const float y = from_bf16(Gp[row * kPPitch + n]);
+                        v = v * (1.0f - y * y);
+                    }
+                    if (nv && m < g.M) {
+                        if (g.Cf) g.Cf[m * g.ldcf + n] = v;
+                        if (g.Cffm) g.Cffm[(int64_t)n * g.ldffm + m] = v;
+                    }
+                    Ap[row * kPPitch + n] = to_bf16(v);
+                }
+        }
+    }
+    if (!g.Crm) return;
+    __syncthreads();
+    const int nc = Nn >> 3;
+    for (int c = tid; c < kPM * nc; c += 256) {
+        const int row = c / nc, col = 8 * (c % nc);
+        const int64_t m = m0 + row;
+        if (m < g.M) *reinterpret_cast<bf16x8*>(g.Crm + m * g.ldc + col) =
+            *reinterpret_cast<const bf16x8*>(Ap + row * kPPitch + col);
+    }
+}
+
+static bool panel_ok(const GemmArgs& g, int splits) {
+    return splits == 1 && !g.partial && !g.Cfm && g.K <= kPK && g.N <= 256 && (g.N % 8) == 0 && (g.ldc % 8) == 0 &&
+           (!g.gate || (g.ldg % 8) == 0) && (reinterpret_cast<uintptr_t>(g.Crm) & 15) == 0 &&
+           (reinterpret_cast<uintptr_t>(g.gate) & 15) == 0;
+}
+
 // ------------------------------------------------------------------ C[O][I] = Y^T X
 // LDS images are [64 samples][128 features] bf16 with 320-B rows: the
 // transposed reads (rows 16kk + 8(g>>1) + q, columns 16(g&1) + 4p of a
@@ -255,6 +375,11 @@ int launch_gemm(const GemmArgs& g0, int splits, float* reduce_out, int accumulat
     DXRL_REQUIRE((reinterpret_cast<uintptr_t>(g.A) & 15) == 0 && (reinterpret_cast<uintptr_t>(g.Bt) & 15) == 0,
                  "gemm: operands must be 16-byte aligned");
     if (splits < 1) splits = 1;
+    if (panel_ok(g, splits)) {
+        g.k_chunk = g.K;
+        hipLaunchKernelGGL(k_gemm_panel, dim3((unsigned)((g.M + kPM - 1) / kPM)), dim3(256), 0, st, g);
+        return launch_check("k_gemm_panel");
+    }
     int64_t chunk = (g.K + splits - 1) / splits;
     chunk = (chunk + kBK - 1) / kBK * kBK;
     splits = (int)((g.K + chunk - 1) / chunk);

@@ -35,9 +35,11 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16* base, int64_t ld, int64_
 }
 
 __device__ __forceinline__ float tanh_f(float x) {
-    // tanh via exp: 1 - 2 / (exp(2x) + 1); saturates cleanly for |x| large
+    // tanh via exp: 1 - 2 / (exp(2x) + 1); saturates cleanly for |x| large.  The
+    // hardware reciprocal (1 ulp) replaces the IEEE division the library's
+    // correctly-rounded-division flag would otherwise emit (network math, not parity math).
     const float e = __expf(2.0f * x);
-    return 1.0f - 2.0f / (e + 1.0f);
+    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
 }
 
 }  // namespace dxrl

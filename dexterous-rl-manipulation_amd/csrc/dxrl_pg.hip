@@ -426,12 +426,27 @@ __global__ __launch_bounds__(256) void k_ppo_heads(HeadArgs h) {
 }
 
 // grads[kOffLogStd + k] = sum_b partial[b][k] - ent_coef  (entropy bonus: d(-c H)/d logstd = -c)
-__global__ void k_logstd_grad(const float* __restrict__ partial, int nb, float ent_coef, float* __restrict__ grads) {
+__global__ __launch_bounds__(256) void k_logstd_grad(const float* __restrict__ partial, int nb, float ent_coef,
+                                                     float* __restrict__ grads) {
+    __shared__ float red[256][kActPad + 1];
+    float s[kActPad];
+#pragma unroll
+    for (int k = 0; k < kActPad; ++k) s[k] = 0.0f;
+    for (int b = threadIdx.x; b < nb; b += 256) {  // fixed partition + fixed tree: deterministic
+#pragma unroll
+        for (int k = 0; k < kActPad; ++k) s[k] += partial[(int64_t)b * kActPad + k];
+    }
+#pragma unroll
+    for (int k = 0; k < kActPad; ++k) red[threadIdx.x][k] = s[k];
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+#pragma unroll
+            for (int k = 0; k < kActPad; ++k) red[threadIdx.x][k] += red[threadIdx.x + w][k];
+        __syncthreads();
+    }
     const int k = threadIdx.x;
-    if (k >= kActPad) return;
-    float s = 0.0f;
-    for (int b = 0; b < nb; ++b) s += partial[(int64_t)b * kActPad + k];
-    grads[kOffLogStd + k] = k < kAct ? s - ent_coef : 0.0f;
+    if (k < kActPad) grads[kOffLogStd + k] = k < kAct ? red[0][k] - ent_coef : 0.0f;
 }
 
 // ------------------------------------------------------------------ optimiser
@@ -601,7 +616,7 @@ int dxrl_pg_heads(int32_t device, const dxrl_pg_heads_args* a, void* stream) {
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_ppo_heads, dim3(nb), dim3(256), 0, st, h);
     if (int rc = launch_check("k_ppo_heads")) return rc;
-    hipLaunchKernelGGL(k_logstd_grad, dim3(1), dim3(64), 0, st, a->dlogstd_partial, nb, (float)a->ent_coef,
+    hipLaunchKernelGGL(k_logstd_grad, dim3(1), dim3(256), 0, st, a->dlogstd_partial, nb, (float)a->ent_coef,
                        a->grads);
     return launch_check("k_logstd_grad");
 }

@@ -30,6 +30,7 @@ import numpy as np
 import torch
 
 from . import _native as N
+from .distributed import all_reduce_sum_
 from .envs import VecEnv
 
 # csrc/dxrl_pg.h
@@ -198,9 +199,7 @@ class PGTrainer:
         self._mlp_forward("a", self.M, self.H1a, self.H2a, head_f32=self.mu)
 
     def _allreduce(self, t):
-        if self.world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+        all_reduce_sum_(t, self.world, self.pg)
 
     def advantages(self):
         c = self.cfg

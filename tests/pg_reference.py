@@ -67,18 +67,24 @@ def gae(rew, done, V, n, T, gamma, lam):
     return adv.reshape(-1), ret.reshape(-1)
 
 
-def loss_and_grads(params, obs_rm, act, logp_old, rew, done, n, T, cfg, bf16=True):
+def loss_and_grads(params, obs_rm, act, logp_old, rew, done, n, T, cfg, bf16=True, norm_stats=None, total=None,
+                   world=1):
     """Manual forward/backward of the PPO objective as the HIP pipeline computes it.
-    Returns (grads [NPARAMS] f32, info dict)."""
+    Sharded use (as PGTrainer with world > 1): norm_stats(adv) -> (mean, std) computed
+    across ranks, total = global sample count, world = number of ranks.
+    Returns (grads [NPARAMS], info dict)."""
     M = n * T
+    total = M if total is None else total
     Wd = unpack(params)
     dt = params.dtype
     X = obs_rm.to(dt)
     H1c, H2c, vhead = mlp_forward(X, Wd, "c", bf16)
     V = vhead[:, 0]
     adv, ret = gae(rew.to(dt), done, V, n, T, cfg["gamma"], cfg["lam"])
-    mean = adv.double().mean()
-    std = adv.double().std()
+    if norm_stats is None:
+        mean, std = adv.double().mean(), adv.double().std()
+    else:
+        mean, std = norm_stats(adv)
     A = ((adv.double() - mean) / (std + 1e-8)).to(dt)
     Xa = X[:M]
     H1a, H2a, muh = mlp_forward(Xa, Wd, "a", bf16)
@@ -91,11 +97,11 @@ def loss_and_grads(params, obs_rm, act, logp_old, rew, done, n, T, cfg, bf16=Tru
     ratio = torch.exp(lp - logp_old)
     s1, s2 = ratio * A, torch.clamp(ratio, 1 - cfg["clip_eps"], 1 + cfg["clip_eps"]) * A
     rc = torch.clamp(ratio, 1 - cfg["clip_eps"], 1 + cfg["clip_eps"])
-    gsel = torch.where((s1 <= s2) | (ratio == rc), -A * ratio, torch.zeros_like(A)) / M
+    gsel = torch.where((s1 <= s2) | (ratio == rc), -A * ratio, torch.zeros_like(A)) / total
     d = a - mu
     dmu = gsel[:, None] * d * iv
-    dls = (gsel[:, None] * (d * d * iv - 1.0)).sum(0) - cfg["ent_coef"]
-    dv = 2.0 * cfg["vf_coef"] * (V[:M] - ret) / M
+    dls = (gsel[:, None] * (d * d * iv - 1.0)).sum(0) - cfg["ent_coef"] / world
+    dv = 2.0 * cfg["vf_coef"] * (V[:M] - ret) / total
     grads = torch.zeros(NPARAMS, dtype=dt, device=params.device)
     G = unpack(grads)
     G["logstd"].copy_(dls)

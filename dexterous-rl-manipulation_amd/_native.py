@@ -73,7 +73,8 @@ class PgRolloutArgs(C.Structure):
     _fields_ = [("horizon", C.c_int32), ("max_steps", C.c_int32), ("policy_seed", C.c_uint64),
                 ("iteration", C.c_uint64), ("obs_noise_std", C.c_double), ("dyn_noise_std", C.c_double)] + \
                [(k, C.c_void_p) for k in ("obs_rm", "obs_fm", "act", "logp", "rew", "done", "ep_return", "ep_count",
-                                          "ep_sum_return", "ep_sum_length", "ep_successes")]
+                                          "ep_sum_return", "ep_sum_length", "ep_successes")] + \
+               [("diag_flags", C.c_int32)]
 
 
 class PgHeadsArgs(C.Structure):

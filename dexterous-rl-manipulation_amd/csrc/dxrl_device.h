@@ -233,6 +233,48 @@ __device__ __forceinline__ void philox_reset_draws(double* d, const dxrl_curricu
         d[kD + k] = rng[k][0] + (rng[k][1] - rng[k][0]) * u01_53(u[2 * (kD + k)], u[2 * (kD + k) + 1]);
 }
 
+// env_reset(philox_reset_draws(...)) without materialising the 21 draws: each
+// Philox block yields two 53-bit uniforms (slots 2b, 2b+1) that are consumed
+// on the spot.  Bit-identical to the two-step form (same slots, same arithmetic).
+__device__ __forceinline__ void env_reset_philox(Env& e, const dxrl_curriculum& cu, uint32_t k0, uint32_t k1,
+                                                 uint64_t ctr) {
+    const bool has = (e.flags & kHasObject) != 0;
+    double spawn[3];
+#pragma unroll
+    for (int b = 0; b < (kReset + 1) / 2; ++b) {
+        const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamReset, (uint32_t)b}, k0, k1);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int k = 2 * b + half;
+            if (k >= kReset) break;
+            const double u = half ? u01_53(r.z, r.w) : u01_53(r.x, r.y);
+            if (k < kD) {
+                e.jp[k] = (float)(-0.1 + (0.1 - -0.1) * u);
+                e.jv[k] = 0.0f;
+            } else if (k == kD + 0) {
+                e.size = cu.has_size_range ? cu.size_range[0] + (cu.size_range[1] - cu.size_range[0]) * u : cu.object_size;
+            } else if (k == kD + 1) {
+                e.mass = cu.has_mass_range ? cu.mass_range[0] + (cu.mass_range[1] - cu.mass_range[0]) * u : cu.object_mass;
+            } else if (k == kD + 2) {
+                e.fric = cu.has_friction_range ? cu.friction_range[0] + (cu.friction_range[1] - cu.friction_range[0]) * u
+                                               : cu.friction_coefficient;
+            } else {
+                const double* rg = k == kD + 3 ? cu.spawn_x_range : (k == kD + 4 ? cu.spawn_y_range : cu.spawn_z_range);
+                spawn[k - kD - 3] = rg[0] + (rg[1] - rg[0]) * u;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        e.op[i] = (double)(float)(has ? e.op[i] : spawn[i]);
+        e.ov[i] = 0.0f;
+    }
+    e.t = 0;
+    e.flags = kOpIsF32 | kHasObject | (cu.friction_is_f64_scalar ? kFricF64 : 0u);
+    double dmin;
+    e.flags |= contacts_of(e, dmin);
+}
+
 __device__ __forceinline__ void write_obs(const Env& e, float* o) {  // ME:254-264
 #pragma unroll
     for (int k = 0; k < kD; ++k) o[k] = e.jp[k];

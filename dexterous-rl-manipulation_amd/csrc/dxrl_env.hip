@@ -58,18 +58,17 @@ __global__ __launch_bounds__(kBlock) void k_reset(EnvSoA s, const uint8_t* __res
     Env e;
     load_env(s, i, e);
     const dxrl_curriculum cu = s.curricula[e.cfg];
-    double d[kReset];
     if (draws) {
+        double d[kReset];
 #pragma unroll
         for (int k = 0; k < kReset; ++k) d[k] = draws[i * kReset + k];
+        env_reset(e, d, cu);
     } else {
         uint32_t k0, k1;
         env_key(seed, gid0 + i, k0, k1);
-        const uint64_t ctr = s.reset_ctr[i];
-        philox_reset_draws(d, cu, k0, k1, ctr);
+        env_reset_philox(e, cu, k0, k1, s.reset_ctr[i]);
     }
     s.reset_ctr[i] += 1;
-    env_reset(e, d, cu);
     store_env(s, i, e);
     if (obs) write_obs(e, obs + i * kObs);
 }

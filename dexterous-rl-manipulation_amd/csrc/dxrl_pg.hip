@@ -68,31 +68,56 @@ struct PgRolloutArgs {
     double* ep_sum_ret;
     int32_t* ep_sum_len;
     int32_t* ep_succ;
+    int diag;       // timing ablations: bit0 skip actor MLP, bit1 skip env step
 };
 
 constexpr int kTile = 64;           // envs per workgroup
 constexpr int kXs = kIn + 8;        // LDS row strides (bf16) -- conflict-free b128 fragment reads
 constexpr int kHs = kH + 8;
 
+// observation element k of ME:254-264 (k is a compile-time constant after unrolling)
+__device__ __forceinline__ float obs_elem(const Env& e, int k) {
+    if (k < kD) return e.jp[k];
+    if (k < 2 * kD) return e.jv[k - kD];
+    if (k < 2 * kD + 3) return (float)e.op[k - 2 * kD];
+    if (k < 2 * kD + 7) return k == 2 * kD + 3 ? 1.0f : 0.0f;  // identity quaternion
+    if (k < 2 * kD + 10) return e.ov[k - 2 * kD - 7];
+    return (float)((e.flags >> (k - 2 * kD - 10)) & 1u);
+}
+
+// Policy input row: obs (+ observation noise, robustness_tests.py:199-207: obs + f32(N(0, s))),
+// streamed 4 elements per Philox block into the bf16 LDS row and the tape.
 __device__ __forceinline__ void write_policy_obs(const Env& e, bf16* xrow, float obs_noise, uint32_t k0, uint32_t k1,
                                                  uint64_t ctr, bf16* tape_rm, bf16* tape_fm, int64_t m,
                                                  int64_t ld_fm) {
-    float o[kObs];
-    write_obs(e, o);
-    if (obs_noise > 0.0f) {  // robustness_tests.py:199-207, obs + f32(N(0, s))
-        float n[kObs];
-        philox_normals<kObs>(n, k0, k1, ctr, kStreamObs);
 #pragma unroll
-        for (int k = 0; k < kObs; ++k) o[k] = o[k] + obs_noise * n[k];
+    for (int b = 0; b < (kObs + 3) / 4; ++b) {
+        float nz[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (obs_noise > 0.0f) {
+            const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamObs, (uint32_t)b}, k0, k1);
+            box_muller(r.x, r.y, nz[0], nz[1]);
+            box_muller(r.z, r.w, nz[2], nz[3]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = 4 * b + q;
+            if (k >= kObs) break;
+            float v = obs_elem(e, k);
+            if (obs_noise > 0.0f) v = v + obs_noise * nz[q];
+            xrow[k] = to_bf16(v);
+        }
     }
-#pragma unroll
-    for (int k = 0; k < kObs; ++k) xrow[k] = to_bf16(o[k]);
     if (tape_rm) {
-        bf16x8 v[kIn / 8];
 #pragma unroll
-        for (int k = 0; k < kIn; ++k) v[k >> 3][k & 7] = k < kObs ? xrow[k] : (k == kObsIn ? (bf16)1.0f : (bf16)0.0f);
+        for (int q = 0; q < kIn / 8; ++q) {
+            bf16x8 v;
 #pragma unroll
-        for (int q = 0; q < kIn / 8; ++q) reinterpret_cast<bf16x8*>(tape_rm + m * kIn)[q] = v[q];
+            for (int j = 0; j < 8; ++j) {
+                const int k = 8 * q + j;
+                v[j] = k < kObs ? xrow[k] : (k == kObsIn ? (bf16)1.0f : (bf16)0.0f);
+            }
+            reinterpret_cast<bf16x8*>(tape_rm + m * kIn)[q] = v;
+        }
     }
     if (tape_fm) {
 #pragma unroll
@@ -100,71 +125,103 @@ __device__ __forceinline__ void write_policy_obs(const Env& e, bf16* xrow, float
     }
 }
 
-// One wave computes a 64-row x 64-col output block of act(A . W^T + b) into LDS.
-// A: LDS [64][lda] bf16; W: global [n][ldw] rows n0..n0+63; K multiple of 16.
-// bias: f32 master column (bias[n * ldb]) -- the same values the training GEMMs use.
-template <int K, bool kTanh>
-__device__ __forceinline__ void wave_layer(const bf16* A, int lda, const bf16* W, int ldw, int n0, const float* bias_p,
+// Register-resident weight fragments: one 32-column N tile of a layer, all of
+// K (K/16 MFMA k-steps): b[k] = W[n0 + r][16k + 8h .. 16k + 8h + 7].  Loaded
+// once per rollout launch, so the per-step MLP reads no weights from memory.
+template <int KS>
+struct WTile {
+    bf16x8 b[KS];
+};
+
+template <int KS>
+__device__ __forceinline__ void load_wtile(WTile<KS>& w, const bf16* W, int ldw, int n0, int lane) {
+    const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) w.b[k] = *reinterpret_cast<const bf16x8*>(W + (int64_t)(n0 + r) * ldw + 16 * k + 8 * h);
+}
+
+// One wave: 64 rows x 32 columns of act(A . W^T + b) into LDS.  A: LDS [64][lda]
+// bf16; the weight fragment of k-step k comes from wfrag(k) (registers or LDS);
+// bias: f32 master column (bias[n * ldb]), the values the training GEMMs use.
+template <int KS, bool kTanh, typename WF>
+__device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfrag, int n0, const float* bias_p,
                                            int ldb, bf16* out, int ldo, int lane) {
     const int r = lane & 31, h = lane >> 5;
-    f32x16 acc[2][2];
+    f32x16 acc[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int q = 0; q < 16; ++q) acc[i][q] = 0.0f;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.0f;
-#pragma unroll 4
-    for (int k = 0; k < K; k += 16) {
-        bf16x8 a[2], b[2];
+    for (int k = 0; k < KS; ++k) {
+        const bf16x8 b = wfrag(k);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const bf16x8*>(A + (32 * i + r) * lda + k + 8 * h);
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            b[j] = *reinterpret_cast<const bf16x8*>(W + (int64_t)(n0 + 32 * j + r) * ldw + k + 8 * h);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+        for (int i = 0; i < 2; ++i) {
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + (32 * i + r) * lda + 16 * k + 8 * h);
+            acc[i] = mfma32(a, b, acc[i]);
+        }
     }
+    const int n = n0 + r;
+    const float bias = bias_p ? bias_p[(int64_t)n * ldb] : 0.0f;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int n = n0 + 32 * j + r;
-        const float bias = bias_p ? bias_p[(int64_t)n * ldb] : 0.0f;
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                float v = acc[i][j][q] + bias;
-                if (kTanh) v = tanh_f(v);
-                out[(32 * i + acc_row(q, lane)) * ldo + (n - n0)] = to_bf16(v);
-            }
-    }
+        for (int q = 0; q < 16; ++q) {
+            float v = acc[i][q] + bias;
+            if (kTanh) v = tanh_f(v);
+            out[(32 * i + acc_row(q, lane)) * ldo + n] = to_bf16(v);
+        }
 }
 
-__global__ __launch_bounds__(256) void k_pg_rollout(PgRolloutArgs p) {
+constexpr int kRolloutWaves = 8;  // 512 threads: wave w owns hidden columns 32w..32w+31
+
+constexpr int kW1s = kIn + 8, kW3s = kH + 8;  // LDS-resident W1 [256][72], W3 [32][264]
+
+__global__ __launch_bounds__(512, 1) void k_pg_rollout(PgRolloutArgs p) {
+    __shared__ __attribute__((aligned(16))) bf16 W1s[kH * kW1s];
+    __shared__ __attribute__((aligned(16))) bf16 W3s[kOut * kW3s];
     __shared__ __attribute__((aligned(16))) bf16 X[kTile * kXs];
     __shared__ __attribute__((aligned(16))) bf16 H1[kTile * kHs];
     __shared__ __attribute__((aligned(16))) bf16 H2[kTile * kHs];
     __shared__ __attribute__((aligned(16))) float MU[kTile * (kOut + 1)];
+    __shared__ float LS[kActPad], SIG[kActPad], ISIG[kActPad];  // log_std, exp(log_std), exp(-log_std)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t n = p.s.n;
     const int64_t i = (int64_t)blockIdx.x * kTile + lane;  // env of this lane (wave 0)
     const bool live = i < n;
     const int64_t T = p.horizon;
-    const bf16* W1 = p.wbf + kBfW1a;
-    const bf16* W2 = p.wbf + kBfW2a;
-    const bf16* W3 = p.wbf + kBfW3a;
+    if (threadIdx.x < kAct) {
+        const float ls = p.params[kOffLogStd + threadIdx.x];
+        LS[threadIdx.x] = ls;
+        SIG[threadIdx.x] = __expf(ls);
+        ISIG[threadIdx.x] = __expf(-ls);
+    }
+    // ---- weights, loaded once per launch: W2 slab in registers (wave w: columns 32w..),
+    //      W1 and the mu head W3 in LDS
+    WTile<kH / 16> w2;
+    load_wtile(w2, p.wbf + kBfW2a, kHx, 32 * wave, lane);
+    for (int c = threadIdx.x; c < kH * (kIn / 8); c += 64 * kRolloutWaves) {
+        const int row = c / (kIn / 8), col = 8 * (c % (kIn / 8));
+        *reinterpret_cast<bf16x8*>(W1s + row * kW1s + col) =
+            *reinterpret_cast<const bf16x8*>(p.wbf + kBfW1a + (int64_t)row * kIn + col);
+    }
+    for (int c = threadIdx.x; c < kOut * (kH / 8); c += 64 * kRolloutWaves) {
+        const int row = c / (kH / 8), col = 8 * (c % (kH / 8));
+        *reinterpret_cast<bf16x8*>(W3s + row * kW3s + col) =
+            *reinterpret_cast<const bf16x8*>(p.wbf + kBfW3a + (int64_t)row * kHx + col);
+    }
+    const int r32 = lane & 31, h2 = lane >> 5;
+    const auto w1frag = [&](int k) {
+        return *reinterpret_cast<const bf16x8*>(W1s + (32 * wave + r32) * kW1s + 16 * k + 8 * h2);
+    };
+    const auto w2frag = [&](int k) { return w2.b[k]; };
     Env e;
-    float logstd[kAct];
     double ep_ret = 0.0;
     int32_t cnt = 0, sum_len = 0, succ = 0;
     double sum_ret = 0.0;
     uint32_t ek0 = 0, ek1 = 0, pk0 = 0, pk1 = 0;
     uint64_t rctr = 0;
     if (wave == 0) {
-#pragma unroll
-        for (int k = 0; k < kAct; ++k) logstd[k] = p.params[kOffLogStd + k];
         // constant padding of the X tile: bias column, zeros
         for (int k = kObs; k < kIn; ++k) X[lane * kXs + k] = k == kObsIn ? (bf16)1.0f : (bf16)0.0f;
         if (live) {
@@ -177,60 +234,71 @@ __global__ __launch_bounds__(256) void k_pg_rollout(PgRolloutArgs p) {
             for (int k = 0; k < kObs; ++k) X[lane * kXs + k] = (bf16)0.0f;
         }
     }
+    const bool mlp = !(p.diag & 1);
     for (int64_t t = 0; t < T; ++t) {
         const int64_t m = t * n + i;
         const uint64_t ctr = p.iteration * (uint64_t)T + (uint64_t)t;
         if (wave == 0 && live)
             write_policy_obs(e, X + lane * kXs, p.obs_noise, pk0, pk1, ctr, p.obs_rm, p.obs_fm, m, T * n);
         __syncthreads();
-        wave_layer<kIn, true>(X, kXs, W1, kIn, 64 * wave, nullptr, 0, H1 + 64 * wave, kHs, lane);  // bias = col 45
+        if (mlp) wave_layer<kIn / 16, true>(X, kXs, w1frag, 32 * wave, nullptr, 0, H1, kHs, lane);  // bias = col 45
         __syncthreads();
-        wave_layer<kH, true>(H1, kHs, W2, kHx, 64 * wave, p.params + kOffW2a + kH, kHx, H2 + 64 * wave, kHs, lane);
+        if (mlp) wave_layer<kH / 16, true>(H1, kHs, w2frag, 32 * wave, p.params + kOffW2a + kH, kHx, H2, kHs, lane);
         __syncthreads();
-        if (wave < 2) {  // mu head: rows 32*wave .. +31, 32 output columns
-            const int r = lane & 31, h = lane >> 5;
+        if (mlp && wave >= 6) {  // mu head: rows 32 (wave - 6) .. +31, 32 output columns
+            const int r = lane & 31, h = lane >> 5, row0 = 32 * (wave - 6);
             f32x16 acc;
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-#pragma unroll 4
-            for (int k = 0; k < kH; k += 16) {
-                const bf16x8 a = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHs + k + 8 * h);
-                const bf16x8 b = *reinterpret_cast<const bf16x8*>(W3 + (int64_t)r * kHx + k + 8 * h);
+#pragma unroll
+            for (int k = 0; k < kH / 16; ++k) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(H2 + (row0 + r) * kHs + 16 * k + 8 * h);
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(W3s + r * kW3s + 16 * k + 8 * h);
                 acc = mfma32(a, b, acc);
             }
             const float bias = p.params[kOffW3a + (int64_t)r * kHx + kH];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) MU[(32 * wave + acc_row(q, lane)) * (kOut + 1) + r] = acc[q] + bias;
+            for (int q = 0; q < 16; ++q) MU[(row0 + acc_row(q, lane)) * (kOut + 1) + r] = acc[q] + bias;
         }
         __syncthreads();
         if (wave == 0 && live) {
-            float mu[kAct], eps[kAct], a[kAct];
+            // a = mu + sigma * eps and log pi(a|s) accumulated in gauss_logp's exact order
+            float a[kAct];
+            float lp = 0.0f;
 #pragma unroll
-            for (int k = 0; k < kAct; ++k) mu[k] = MU[lane * (kOut + 1) + k];
-            philox_normals<kAct>(eps, pk0, pk1, ctr, kStreamPolicy);
+            for (int b = 0; b < (kAct + 3) / 4; ++b) {
+                const u32x4 rr = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamPolicy, (uint32_t)b},
+                                        pk0, pk1);
+                float nz[4];
+                box_muller(rr.x, rr.y, nz[0], nz[1]);
+                box_muller(rr.z, rr.w, nz[2], nz[3]);
 #pragma unroll
-            for (int k = 0; k < kAct; ++k) a[k] = mu[k] + __expf(logstd[k]) * eps[k];
-            p.logp[m] = gauss_logp(a, mu, logstd);
+                for (int q = 0; q < 4; ++q) {
+                    const int k = 4 * b + q;
+                    if (k >= kAct) break;
+                    const float mu = mlp ? MU[lane * (kOut + 1) + k] : 0.0f;
+                    a[k] = mu + SIG[k] * nz[q];
+                    const float z = (a[k] - mu) * ISIG[k];
+                    lp += -0.5f * z * z - LS[k] - 0.5f * kLog2Pi;
+                }
+            }
+            p.logp[m] = lp;
             float4* arow = reinterpret_cast<float4*>(p.act + m * kActPad);
             arow[0] = float4{a[0], a[1], a[2], a[3]};
             arow[1] = float4{a[4], a[5], a[6], a[7]};
             arow[2] = float4{a[8], a[9], a[10], a[11]};
             arow[3] = float4{a[12], a[13], a[14], 0.0f};
-            float ae[kAct];
-            if (p.dyn_noise > 0.0f) {  // robustness_tests.py:180-187
+            if (p.dyn_noise > 0.0f) {  // robustness_tests.py:180-187 (the tape keeps the policy's action)
                 float dn[kAct];
                 philox_normals<kAct>(dn, pk0, pk1, ctr, kStreamDyn);
 #pragma unroll
-                for (int k = 0; k < kAct; ++k) ae[k] = clipf(a[k] + p.dyn_noise * dn[k], -1.0f, 1.0f);
-            } else {
-#pragma unroll
-                for (int k = 0; k < kAct; ++k) ae[k] = a[k];
+                for (int k = 0; k < kAct; ++k) a[k] = clipf(a[k] + p.dyn_noise * dn[k], -1.0f, 1.0f);
             }
-            bool te, tr;
-            double cp[4];
-            const double r = env_step(e, ae, true, p.w, p.max_episode_steps, te, tr, cp);
+            bool te = false, tr = false;
+            double cp[4], r = 0.0;
+            if (!(p.diag & 2)) r = env_step(e, a, true, p.w, p.max_episode_steps, te, tr, cp);
             ep_ret += r;
-            const bool d = te || tr || e.t >= p.max_steps;
+            const bool d = !(p.diag & 2) && (te || tr || e.t >= p.max_steps);
             p.rew[m] = (float)r;
             p.done[m] = d;
             if (d) {
@@ -238,11 +306,8 @@ __global__ __launch_bounds__(256) void k_pg_rollout(PgRolloutArgs p) {
                 sum_ret += ep_ret;
                 sum_len += e.t;
                 succ += te;
-                const dxrl_curriculum cu = p.s.curricula[e.cfg];
-                double dr[kReset];
-                philox_reset_draws(dr, cu, ek0, ek1, rctr);
+                env_reset_philox(e, p.s.curricula[e.cfg], ek0, ek1, rctr);
                 ++rctr;
-                env_reset(e, dr, cu);
                 ep_ret = 0.0;
             }
         }
@@ -568,10 +633,12 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                     a->ep_count,
                     a->ep_sum_return,
                     a->ep_sum_length,
-                    a->ep_successes};
+                    a->ep_successes,
+                    a->diag_flags};
     DeviceGuard g(env->device);
     const int64_t n = env->cfg.num_envs;
-    hipLaunchKernelGGL(k_pg_rollout, dim3((unsigned)((n + kTile - 1) / kTile)), dim3(256), 0, as_stream(stream), p);
+    hipLaunchKernelGGL(k_pg_rollout, dim3((unsigned)((n + kTile - 1) / kTile)), dim3(64 * kRolloutWaves), 0,
+                       as_stream(stream), p);
     return launch_check("k_pg_rollout");
 }
 

@@ -187,20 +187,20 @@ __global__ __launch_bounds__(64) void k_rollout_simple(EnvSoA s, LearnerSoA L, R
             }
             // next run_episode: env.reset() (no seed) + policy.reset()
             const dxrl_curriculum cu = s.curricula[e.cfg];
-            double d[kReset];
             if (kTape) {
                 if ((int64_t)(done_eps + 1) * kReset > io.reset_stride) {
                     ok = false;
                     break;
                 }
+                double d[kReset];
 #pragma unroll
                 for (int k = 0; k < kReset; ++k) d[k] = rrow[done_eps * kReset + k];
+                env_reset(e, d, cu);
             } else {
-                philox_reset_draws(d, cu, ek0, ek1, rctr);
+                env_reset_philox(e, cu, ek0, ek1, rctr);
             }
             ++rctr;
             ++done_eps;
-            env_reset(e, d, cu);
             best = -__builtin_inf();
             ep_ret = 0.0;
         }

@@ -92,6 +92,7 @@ class PGTrainer:
         self.world = world_size
         self.step_count = 0
         self.iteration_index = 0
+        self.diag_flags = 0  # rollout timing ablations only (see dxrl_pg_rollout_args.diag_flags)
         d, f32, bf, M, n, T = self.dev, torch.float32, torch.bfloat16, self.M, self.n, self.T
         z = lambda *s, dt=f32: torch.zeros(*s, dtype=dt, device=d)  # noqa: E731
         self.params, self.grads, self.m1, self.m2 = z(NPARAMS), z(NPARAMS), z(NPARAMS), z(NPARAMS)
@@ -181,6 +182,7 @@ class PGTrainer:
                                                             p(self.rew), p(self.done))
         a.ep_return, a.ep_count, a.ep_sum_return = p(self.ep_ret), p(self.ep_count), p(self.ep_sum_ret)
         a.ep_sum_length, a.ep_successes = p(self.ep_sum_len), p(self.ep_succ)
+        a.diag_flags = self.diag_flags
         N.call("dxrl_pg_rollout", self.env.handle, p(self.packed), p(self.params), C.byref(a), self._s())
 
     def _mlp_forward(self, net, rows, H1, H2, head_f32=None, head_fm=None, ld_head_fm=0):

@@ -238,6 +238,8 @@ typedef struct dxrl_pg_rollout_args {
     double* ep_sum_return;     /* f64 [N]                                                  */
     int32_t* ep_sum_length;    /* i32 [N]                                                  */
     int32_t* ep_successes;     /* i32 [N] finished episodes that terminated (>= 3 contacts) */
+    int32_t diag_flags;        /* diagnostics only (timing ablations): bit0 skip the actor MLP
+                                  (mu = 0), bit1 skip the env step; 0 in every real run      */
 } dxrl_pg_rollout_args;
 
 /* Fused policy + env rollout: T steps of actor MLP (bf16 MFMA) -> Gaussian

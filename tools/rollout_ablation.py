@@ -1,0 +1,26 @@
+"""Time the fused PG rollout with parts switched off (diag flags) at the bench shape."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import dexterous_rl_manipulation_amd as pkg  # noqa: E402
+from dexterous_rl_manipulation_amd import envs, trainer  # noqa: E402
+
+dev = torch.device("cuda:0")
+for cur in ("easy", "hard"):
+    env = envs.VecEnv(4096, curriculum_config=pkg.CurriculumConfig.named(cur), reward_type="dense", seed=1, device=dev)
+    tr = trainer.PGTrainer(env, trainer.TrainerConfig(horizon=200, seed=7))
+    env.reset(write_obs=False)
+    for flags, name in ((0, "full"), (1, "no-MLP"), (2, "no-env"), (3, "neither")):
+        tr.diag_flags = flags
+        tr.rollout()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(5):
+            tr.rollout()
+        b.record()
+        torch.cuda.synchronize()
+        print(f"{cur:5s} {name:8s} {a.elapsed_time(b) / 5:8.3f} ms")

@@ -140,44 +140,54 @@ __device__ __forceinline__ void load_wtile(WTile<KS>& w, const bf16* W, int ldw,
     for (int k = 0; k < KS; ++k) w.b[k] = *reinterpret_cast<const bf16x8*>(W + (int64_t)(n0 + r) * ldw + 16 * k + 8 * h);
 }
 
-// One wave: 64 rows x 32 columns of act(A . W^T + b) into LDS.  A: LDS [64][lda]
-// bf16; the weight fragment of k-step k comes from wfrag(k) (registers or LDS);
-// bias: f32 master column (bias[n * ldb]), the values the training GEMMs use.
-template <int KS, bool kTanh, typename WF>
+// One wave: 64 rows x 32*NT columns of act(A . W^T + b) into LDS.  A: LDS [64][lda]
+// bf16; the weight fragment of N-tile j, k-step k comes from wfrag(j, k) (registers
+// or LDS); bias: f32 master column (bias[n * ldb]), the values the training GEMMs use.
+template <int KS, int NT, bool kTanh, typename WF>
 __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfrag, int n0, const float* bias_p,
                                            int ldb, bf16* out, int ldo, int lane) {
     const int r = lane & 31, h = lane >> 5;
-    f32x16 acc[2];
+    f32x16 acc[2][NT];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) acc[i][q] = 0.0f;
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.0f;
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
-        const bf16x8 b = wfrag(k);
+        bf16x8 a[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + (32 * i + r) * lda + 16 * k + 8 * h);
-            acc[i] = mfma32(a, b, acc[i]);
+        for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const bf16x8*>(A + (32 * i + r) * lda + 16 * k + 8 * h);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const bf16x8 b = wfrag(j, k);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) acc[i][j] = mfma32(a[i], b, acc[i][j]);
         }
     }
-    const int n = n0 + r;
-    const float bias = bias_p ? bias_p[(int64_t)n * ldb] : 0.0f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < NT; ++j) {
+        const int n = n0 + 32 * j + r;
+        const float bias = bias_p ? bias_p[(int64_t)n * ldb] : 0.0f;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            float v = acc[i][q] + bias;
-            if (kTanh) v = tanh_f(v);
-            out[(32 * i + acc_row(q, lane)) * ldo + n] = to_bf16(v);
-        }
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                float v = acc[i][j][q] + bias;
+                if (kTanh) v = tanh_f(v);
+                out[(32 * i + acc_row(q, lane)) * ldo + n] = to_bf16(v);
+            }
+    }
 }
 
-constexpr int kRolloutWaves = 8;  // 512 threads: wave w owns hidden columns 32w..32w+31
+// 4 waves (one per SIMD, so a wave may use 256 VGPRs + 256 AGPRs): wave w owns hidden
+// columns kCpw*w .. kCpw*w + kCpw - 1 of both hidden layers; waves 2, 3 compute the mu head.
+constexpr int kRolloutWaves = 4, kCpw = kH / kRolloutWaves, kNT = kCpw / 32;
 
 constexpr int kW1s = kIn + 8, kW3s = kH + 8;  // LDS-resident W1 [256][72], W3 [32][264]
 
-__global__ __launch_bounds__(512, 1) void k_pg_rollout(PgRolloutArgs p) {
+__global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout(PgRolloutArgs p) {
     __shared__ __attribute__((aligned(16))) bf16 W1s[kH * kW1s];
     __shared__ __attribute__((aligned(16))) bf16 W3s[kOut * kW3s];
     __shared__ __attribute__((aligned(16))) bf16 X[kTile * kXs];
@@ -198,8 +208,9 @@ __global__ __launch_bounds__(512, 1) void k_pg_rollout(PgRolloutArgs p) {
     }
     // ---- weights, loaded once per launch: W2 slab in registers (wave w: columns 32w..),
     //      W1 and the mu head W3 in LDS
-    WTile<kH / 16> w2;
-    load_wtile(w2, p.wbf + kBfW2a, kHx, 32 * wave, lane);
+    WTile<kH / 16> w2[kNT];
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) load_wtile(w2[j], p.wbf + kBfW2a, kHx, kCpw * wave + 32 * j, lane);
     for (int c = threadIdx.x; c < kH * (kIn / 8); c += 64 * kRolloutWaves) {
         const int row = c / (kIn / 8), col = 8 * (c % (kIn / 8));
         *reinterpret_cast<bf16x8*>(W1s + row * kW1s + col) =
@@ -211,10 +222,10 @@ __global__ __launch_bounds__(512, 1) void k_pg_rollout(PgRolloutArgs p) {
             *reinterpret_cast<const bf16x8*>(p.wbf + kBfW3a + (int64_t)row * kHx + col);
     }
     const int r32 = lane & 31, h2 = lane >> 5;
-    const auto w1frag = [&](int k) {
-        return *reinterpret_cast<const bf16x8*>(W1s + (32 * wave + r32) * kW1s + 16 * k + 8 * h2);
+    const auto w1frag = [&](int j, int k) {
+        return *reinterpret_cast<const bf16x8*>(W1s + (kCpw * wave + 32 * j + r32) * kW1s + 16 * k + 8 * h2);
     };
-    const auto w2frag = [&](int k) { return w2.b[k]; };
+    const auto w2frag = [&](int j, int k) { return w2[j].b[k]; };
     Env e;
     double ep_ret = 0.0;
     int32_t cnt = 0, sum_len = 0, succ = 0;
@@ -241,12 +252,13 @@ __global__ __launch_bounds__(512, 1) void k_pg_rollout(PgRolloutArgs p) {
         if (wave == 0 && live)
             write_policy_obs(e, X + lane * kXs, p.obs_noise, pk0, pk1, ctr, p.obs_rm, p.obs_fm, m, T * n);
         __syncthreads();
-        if (mlp) wave_layer<kIn / 16, true>(X, kXs, w1frag, 32 * wave, nullptr, 0, H1, kHs, lane);  // bias = col 45
+        if (mlp) wave_layer<kIn / 16, kNT, true>(X, kXs, w1frag, kCpw * wave, nullptr, 0, H1, kHs, lane);  // b: col 45
         __syncthreads();
-        if (mlp) wave_layer<kH / 16, true>(H1, kHs, w2frag, 32 * wave, p.params + kOffW2a + kH, kHx, H2, kHs, lane);
+        if (mlp)
+            wave_layer<kH / 16, kNT, true>(H1, kHs, w2frag, kCpw * wave, p.params + kOffW2a + kH, kHx, H2, kHs, lane);
         __syncthreads();
-        if (mlp && wave >= 6) {  // mu head: rows 32 (wave - 6) .. +31, 32 output columns
-            const int r = lane & 31, h = lane >> 5, row0 = 32 * (wave - 6);
+        if (mlp && wave >= kRolloutWaves - 2) {  // mu head: 32 rows per wave, 32 output columns
+            const int r = lane & 31, h = lane >> 5, row0 = 32 * (wave - (kRolloutWaves - 2));
             f32x16 acc;
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[q] = 0.0f;

@@ -42,14 +42,29 @@ PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 STEP_BYTES_PER_ENV = 594  # k_step algorithmic bytes per env-step
 
 
+# BASELINE.json configs[1..4] as PG workloads (configs[0] is the CPU plumbing case)
+WORKLOADS = {
+    "easy": {"envs": 4096, "curriculum": "easy", "desc": "config_easy.json"},
+    "default": {"envs": 4096, "curriculum": "easy", "scheduler": True,
+                "desc": "config_default.json (CurriculumScheduler easy->hard fed by per-episode records)"},
+    "hard_heldout": {"envs": 8192, "curriculum": "hard", "heldout": True,
+                     "desc": "config_hard.json + HeldOutObjectSet table (env i -> object i % 10)"},
+    "variable_noise": {"envs": 4096, "curriculum": "variable", "obs_noise": 0.05, "dyn_noise": 0.05,
+                       "desc": "config_variable.json + fused obs/dynamics noise 0.05"},
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    p.add_argument("--config", choices=sorted(WORKLOADS), default="easy",
+                   help="BASELINE configs[1..4]: easy (C2, the metric's config), default (C3: curriculum "
+                        "scheduler), hard_heldout (C4: held-out object table, 8192 envs), variable_noise (C5)")
+    p.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's)")
     p.add_argument("--horizon", type=int, default=200, help="env steps per bench step (rollout length)")
-    p.add_argument("--curriculum", default="easy")
+    p.add_argument("--curriculum", default=None, help="override the config's curriculum preset")
     p.add_argument("--learner", choices=["pg", "simple"], default="pg",
                    help="pg: MLP actor-critic policy-gradient iteration (default); simple: SimpleLearner rollout")
     p.add_argument("--roofline-envs", type=int, default=1 << 22)
@@ -57,7 +72,11 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
-    return p.parse_args()
+    a = p.parse_args()
+    w = WORKLOADS[a.config]
+    a.envs = a.envs or w["envs"]
+    a.curriculum = a.curriculum or w["curriculum"]
+    return a
 
 
 def dist_setup(args):
@@ -102,14 +121,29 @@ def pg_bench(args, world, rank, dev):
     import dexterous_rl_manipulation_amd as pkg
     from dexterous_rl_manipulation_amd import envs, trainer
     n = args.envs
+    w = WORKLOADS[args.config]
     env = envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.named(args.curriculum), reward_type="dense",
                       seed=20240601, device=dev, global_env_offset=rank * n)
+    if w.get("heldout"):
+        from dexterous_rl_manipulation_amd import evaluation
+        ex = pkg.experiments.load_named_config("default")
+        hs = evaluation.HeldOutObjectSet(pkg.CurriculumConfig.named(args.curriculum),
+                                         num_heldout_objects=ex.evaluation.num_heldout_objects, seed=ex.evaluation.seed)
+        cfgs, idx = hs.native_table(n)
+        env.set_curricula(cfgs, env_index=(idx + rank * n) % len(cfgs))
     pg = None
     if world > 1:
         import torch.distributed as dist
         pg = dist.group.WORLD
-    tr = trainer.PGTrainer(env, trainer.TrainerConfig(horizon=args.horizon, seed=7), process_group=pg,
-                           world_size=world)
+    tcfg = trainer.TrainerConfig(horizon=args.horizon, seed=7, obs_noise_std=w.get("obs_noise", 0.0),
+                                 dyn_noise_std=w.get("dyn_noise", 0.0), record_cap=16 if w.get("scheduler") else 0)
+    tr = trainer.PGTrainer(env, tcfg, process_group=pg, world_size=world)
+    if w.get("scheduler"):
+        sc = pkg.experiments.load_named_config("default").curriculum_scheduler
+        C = pkg.CurriculumConfig
+        tr.attach_curriculum(pkg.experiments.CurriculumScheduler(
+            C.named(sc.initial_difficulty), C.named(sc.target_difficulty), sc.success_rate_threshold,
+            sc.min_episodes_before_progression, sc.window_size, sc.progression_steps))
     env.reset(write_obs=False)
     for _ in range(args.warmup):
         tr.iteration()
@@ -126,6 +160,8 @@ def pg_bench(args, world, rank, dev):
     # phase breakdown (one extra iteration, outside the timed region)
     stream = torch.cuda.current_stream(dev)
     names = ["rollout", "critic_forward", "advantages", "actor_forward", "heads", "backward", "optimizer_step"]
+    if tr.scheduler is not None:
+        names.append("_feed_scheduler")  # records D2H + CurriculumScheduler.update_batch + table push
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
     evs[0].record(stream)
     for k, nm in enumerate(names):
@@ -143,6 +179,9 @@ def pg_bench(args, world, rank, dev):
                                               "train_bwd": BWD_BOTH}}
     mfma["frac"] = round(mfma["training_gemms_achieved"] / PEAK_BF16_TFS, 4)
     stats = tr.episode_stats()
+    if tr.scheduler is not None:
+        stats["curriculum_level"] = tr.scheduler.get_difficulty_level()
+        stats["scheduler_episodes"] = tr.scheduler.total_episodes
     stats.update({k: round(v, 5) for k, v in tr.loss_stats().items()})
     return wall, phases, mfma, stats
 
@@ -257,7 +296,7 @@ def main():
     extra = {}
     if args.learner == "pg":
         wall, phases, mfma, stats = pg_bench(args, world, rank, dev)
-        workload = (f"config_{args.curriculum}.json PG iteration: fused actor-MLP(256,256) rollout of "
+        workload = (f"{WORKLOADS[args.config]['desc']} PG iteration: fused actor-MLP(256,256) rollout of "
                     f"{args.horizon} env steps x {args.envs} envs + critic fwd + GAE + adv-norm + PPO heads + "
                     f"backward + Adam")
         dtype = "bf16 MFMA (f32 acc) + f32/f64 env"

@@ -74,7 +74,9 @@ class PgRolloutArgs(C.Structure):
                 ("iteration", C.c_uint64), ("obs_noise_std", C.c_double), ("dyn_noise_std", C.c_double)] + \
                [(k, C.c_void_p) for k in ("obs_rm", "obs_fm", "act", "logp", "rew", "done", "ep_return", "ep_count",
                                           "ep_sum_return", "ep_sum_length", "ep_successes")] + \
-               [("diag_flags", C.c_int32)]
+               [("diag_flags", C.c_int32), ("success_rule", C.c_int32), ("record_cap", C.c_int32),
+                ("rec_return", C.c_void_p), ("rec_length", C.c_void_p), ("rec_success", C.c_void_p),
+                ("rec_end_step", C.c_void_p)]
 
 
 class PgHeadsArgs(C.Structure):

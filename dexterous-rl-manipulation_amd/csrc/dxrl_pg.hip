@@ -69,6 +69,12 @@ struct PgRolloutArgs {
     int32_t* ep_sum_len;
     int32_t* ep_succ;
     int diag;       // timing ablations: bit0 skip actor MLP, bit1 skip env step
+    int success_terminated;
+    int record_cap;
+    double* rec_return;
+    int32_t* rec_length;
+    uint8_t* rec_success;
+    int32_t* rec_end_step;
 };
 
 constexpr int kTile = 64;           // envs per workgroup
@@ -314,6 +320,13 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout(PgRolloutA
             p.rew[m] = (float)r;
             p.done[m] = d;
             if (d) {
+                if (cnt < p.record_cap) {
+                    const int64_t o = i * p.record_cap + cnt;
+                    p.rec_return[o] = ep_ret;
+                    p.rec_length[o] = e.t;
+                    p.rec_success[o] = p.success_terminated ? (uint8_t)te : (uint8_t)0;
+                    p.rec_end_step[o] = (int32_t)t;
+                }
                 ++cnt;
                 sum_ret += ep_ret;
                 sum_len += e.t;
@@ -622,6 +635,8 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                      a->ep_sum_return && a->ep_sum_length && a->ep_successes,
                  "null tape / episode buffer");
     DXRL_REQUIRE(env->cfg.reward_type == DXRL_REWARD_DENSE, "the policy-gradient rollout uses the dense reward");
+    DXRL_REQUIRE(a->record_cap == 0 || (a->rec_return && a->rec_length && a->rec_success && a->rec_end_step),
+                 "record_cap > 0 needs all four record buffers");
     PgRolloutArgs p{env->soa,
                     weights_of(env->cfg),
                     env->cfg.max_episode_steps,
@@ -646,7 +661,13 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                     a->ep_sum_return,
                     a->ep_sum_length,
                     a->ep_successes,
-                    a->diag_flags};
+                    a->diag_flags,
+                    a->success_rule == DXRL_SUCCESS_TERMINATED,
+                    a->record_cap,
+                    a->rec_return,
+                    a->rec_length,
+                    a->rec_success,
+                    a->rec_end_step};
     DeviceGuard g(env->device);
     const int64_t n = env->cfg.num_envs;
     hipLaunchKernelGGL(k_pg_rollout, dim3((unsigned)((n + kTile - 1) / kTile)), dim3(64 * kRolloutWaves), 0,

@@ -184,6 +184,48 @@ class CurriculumScheduler:
         self.total_episodes += 1
         return self._progress() if self._should_progress() else False
 
+    def update_batch(self, successes, episode_steps) -> bool:
+        """Exactly ``any([self.update(s, n) for s, n in zip(successes, episode_steps)])`` --
+        same lists, totals, progression points and history entries -- without a Python call
+        per episode (a 4096-env iteration finishes thousands of episodes).  The progression
+        test depends only on the success window and the totals, so every candidate index is
+        found with one cumulative sum; the difficulty only caps how many of them fire."""
+        s = np.asarray(successes, dtype=bool).ravel()
+        st = np.asarray(episode_steps, dtype=np.int64).ravel()
+        if s.shape != st.shape:
+            raise ValueError("successes and episode_steps must have the same length")
+        n = s.size
+        if n == 0:
+            return False
+        w = self.window_size
+        if w <= 0 or type(self).update is not CurriculumScheduler.update:  # other rules: per-episode calls
+            return any([self.update(bool(a), int(b)) for a, b in zip(s, st)])
+        base = len(self.episode_successes)
+        tail = np.asarray(self.episode_successes[-w:] if w > 0 else [], dtype=bool)
+        hist = np.concatenate([tail, s])
+        csum = np.concatenate([[0], np.cumsum(hist, dtype=np.int64)])
+        k = np.arange(n)
+        end = tail.size + k + 1                                     # hist prefix length after s[k]
+        cnt = csum[end] - csum[np.maximum(end - w, 0)]
+        ok = ((self.total_episodes + k + 1 >= self.min_episodes_before_progression) & (base + k + 1 >= w)
+              & (cnt / w >= self.success_rate_threshold))
+        steps_cum = np.cumsum(st)
+        done, progressed = 0, False
+        for j in np.nonzero(ok)[0]:
+            if self.current_difficulty_level >= 1.0:
+                break
+            self.episode_successes.extend(s[done:j + 1].tolist())
+            self.episode_steps.extend(st[done:j + 1].tolist())
+            self.total_steps += int(steps_cum[j] - (steps_cum[done - 1] if done else 0))
+            self.total_episodes += j + 1 - done
+            done = j + 1
+            progressed |= self._progress()
+        self.episode_successes.extend(s[done:].tolist())
+        self.episode_steps.extend(st[done:].tolist())
+        self.total_steps += int(steps_cum[-1] - (steps_cum[done - 1] if done else 0))
+        self.total_episodes += n - done
+        return progressed
+
     def _window_rate(self):
         return np.mean(self.episode_successes[-self.window_size:])
 

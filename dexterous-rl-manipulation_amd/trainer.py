@@ -71,6 +71,8 @@ class TrainerConfig:
     dyn_noise_std: float = 0.0               # config C5: 0.05
     seed: int = 0
     splitk_target_blocks: int = 768
+    record_cap: int = 0                      # per-env episode records per iteration (0 = off)
+    success_rule: str = "terminated"         # "training" (episode_utils.py:52) or "terminated"
 
 
 class PGTrainer:
@@ -108,6 +110,14 @@ class PGTrainer:
         self.ep_sum_ret = torch.zeros(n, dtype=torch.float64, device=d)
         self.ep_sum_len = z(n, dt=torch.int32)
         self.ep_succ = z(n, dt=torch.int32)
+        cap = max(0, int(cfg.record_cap))
+        self.rec_return = torch.zeros(n, max(cap, 1), dtype=torch.float64, device=d)
+        self.rec_length = z(n, max(cap, 1), dt=torch.int32)
+        self.rec_success = z(n, max(cap, 1), dt=torch.uint8)
+        self.rec_end = z(n, max(cap, 1), dt=torch.int32)
+        if cfg.success_rule not in ("training", "terminated"):
+            raise ValueError("success_rule must be 'training' or 'terminated'")
+        self.scheduler = None
         # hidden activations, row-major [rows][288]: columns 0..255 = tanh units, column 256 = 1
         # (the next layer reads K = 256; the weight-gradient GEMM reads I = 288 and gets the bias
         # gradient as column 256)
@@ -183,6 +193,10 @@ class PGTrainer:
         a.ep_return, a.ep_count, a.ep_sum_return = p(self.ep_ret), p(self.ep_count), p(self.ep_sum_ret)
         a.ep_sum_length, a.ep_successes = p(self.ep_sum_len), p(self.ep_succ)
         a.diag_flags = self.diag_flags
+        a.success_rule = N.SUCCESS_TERMINATED if self.cfg.success_rule == "terminated" else N.SUCCESS_TRAINING
+        a.record_cap = max(0, int(self.cfg.record_cap))
+        a.rec_return, a.rec_length = p(self.rec_return), p(self.rec_length)
+        a.rec_success, a.rec_end_step = p(self.rec_success), p(self.rec_end)
         N.call("dxrl_pg_rollout", self.env.handle, p(self.packed), p(self.params), C.byref(a), self._s())
 
     def _mlp_forward(self, net, rows, H1, H2, head_f32=None, head_fm=None, ld_head_fm=0):
@@ -247,6 +261,27 @@ class PGTrainer:
                c.max_grad_norm, self._s())
         self.pack()
 
+    def attach_curriculum(self, scheduler):
+        """Host-side CurriculumScheduler (experiments/curriculum_scheduler.py) fed with this
+        iteration's finished episodes in (end step, global env id) order; a progression pushes
+        the new config into the device table (effective at each env's next reset, as
+        evaluation/component_ablation.py:165-166 does between episodes)."""
+        if self.cfg.record_cap <= 0:
+            raise ValueError("attach_curriculum needs TrainerConfig.record_cap > 0")
+        self.scheduler = scheduler
+        self.env.set_curriculum(scheduler.get_current_config())
+
+    def episode_records(self):
+        from .training import gather_records
+        return gather_records(self.ep_count, self.cfg.record_cap, self.rec_return, self.rec_length,
+                              self.rec_success, self.rec_end, self.env._cfg.global_env_offset)
+
+    def _feed_scheduler(self):
+        rec = self.episode_records()
+        if self.scheduler.update_batch(rec.success, rec.steps):
+            self.env.set_curriculum(self.scheduler.get_current_config())
+        return rec
+
     def iteration(self, update: bool = True):
         self.rollout()
         self.critic_forward()
@@ -256,6 +291,8 @@ class PGTrainer:
         self.backward()
         if update:
             self.optimizer_step()
+        if self.scheduler is not None:
+            self._feed_scheduler()
         self.iteration_index += 1
 
     # ------------------------------------------------------------------ stats

@@ -195,16 +195,20 @@ class SimpleLearnerRollout:
         return self.records()
 
     def records(self) -> EpisodeRecords:
-        counts = self.ep_count.cpu().numpy().astype(np.int64)
-        kept = np.minimum(counts, self.record_cap)
-        n = self.env.num_envs
-        cols = np.arange(self.record_cap)[None, :]
-        m = cols < kept[:, None]
-        env_id = np.broadcast_to(np.arange(n)[:, None] + self.env._cfg.global_env_offset, m.shape)[m]
-        end = self.ep_end.cpu().numpy()[m]
-        order = np.lexsort((env_id, end))
-        return EpisodeRecords(env_id=env_id[order], end_step=end[order],
-                              total_reward=self.ep_return.cpu().numpy()[m][order],
-                              steps=self.ep_length.cpu().numpy()[m][order],
-                              success=self.ep_success.cpu().numpy()[m][order].astype(bool),
-                              dropped=int((counts - kept).sum()))
+        return gather_records(self.ep_count, self.record_cap, self.ep_return, self.ep_length, self.ep_success,
+                              self.ep_end, self.env._cfg.global_env_offset)
+
+
+def gather_records(count, cap, ret, length, success, end_step, gid0=0) -> EpisodeRecords:
+    """Device [N][cap] episode records -> host EpisodeRecords in (end step, global env id)
+    order, the order the host-side CurriculumScheduler is fed in."""
+    counts = count.cpu().numpy().astype(np.int64)
+    kept = np.minimum(counts, cap)
+    n = counts.shape[0]
+    m = np.arange(cap)[None, :] < kept[:, None]
+    env_id = np.broadcast_to(np.arange(n)[:, None] + gid0, m.shape)[m]
+    end = end_step.cpu().numpy()[m]
+    order = np.lexsort((env_id, end))
+    return EpisodeRecords(env_id=env_id[order], end_step=end[order], total_reward=ret.cpu().numpy()[m][order],
+                          steps=length.cpu().numpy()[m][order],
+                          success=success.cpu().numpy()[m][order].astype(bool), dropped=int((counts - kept).sum()))

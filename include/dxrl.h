@@ -240,6 +240,12 @@ typedef struct dxrl_pg_rollout_args {
     int32_t* ep_successes;     /* i32 [N] finished episodes that terminated (>= 3 contacts) */
     int32_t diag_flags;        /* diagnostics only (timing ablations): bit0 skip the actor MLP
                                   (mu = 0), bit1 skip the env step; 0 in every real run      */
+    int32_t success_rule;      /* DXRL_SUCCESS_* for the episode records                   */
+    int32_t record_cap;        /* per-env episode records [N][record_cap] (0 = none)       */
+    double* rec_return;
+    int32_t* rec_length;
+    uint8_t* rec_success;
+    int32_t* rec_end_step;     /* step index t within this call                            */
 } dxrl_pg_rollout_args;
 
 /* Fused policy + env rollout: T steps of actor MLP (bf16 MFMA) -> Gaussian

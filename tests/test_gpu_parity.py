@@ -330,3 +330,22 @@ def test_noise_wrapper_on_facade(pkg, ci):
             obs, r, te, tr, _ = env.step(z["actions"][e, t])
             assert np.array_equal(obs, z["obs"][e, t]), (e, t)
             assert math.isclose(r, z["reward"][e, t], rel_tol=REW_RTOL, abs_tol=1e-15)
+
+
+def test_heldout_table_on_device(pkg):
+    """Config C4: HeldOutObjectSet (heldout_objects.py:39-189) as the device curricula table --
+    env i resets to held-out object i % 20 exactly (scalar size/mass/friction, f64 in the slab)."""
+    ev = pkg.evaluation
+    hs = ev.HeldOutObjectSet(pkg.experiments.CurriculumConfig.hard(), seed=42)
+    n = 1000
+    env = pkg.envs.VecEnv(n, reward_type="dense", seed=9)
+    cfgs, idx = hs.native_table(n)
+    env.set_curricula(cfgs, env_index=idx)
+    env.reset(write_obs=False)
+    size, mass, fric = (t.cpu().numpy() for t in (env.object_size, env.object_mass, env.friction_coefficient))
+    for i in (0, 1, 19, 20, 537, n - 1):
+        o = hs.heldout_objects[i % len(hs.heldout_objects)]
+        assert (size[i], mass[i], fric[i]) == (o.size, o.mass, o.friction), i
+    # a step on the held-out table advances without error and keeps the per-env objects
+    env.step(torch.zeros(n, 15, device=env.device))
+    assert np.array_equal(env.object_size.cpu().numpy(), size)

@@ -159,3 +159,85 @@ def test_training_runs_and_moves(pkg):
     assert all(math.isfinite(v) for v in s.values())
     st = tr.episode_stats()
     assert st["env_steps"] == 512 * 64
+
+
+def test_episode_records_match_tape(pkg):
+    """Per-episode records (feeds CurriculumScheduler, curriculum_scheduler.py:116) agree with the
+    done/reward tape: one record per done flag, end step, length, f64 return."""
+    n, T, cap = 64, 40, 8
+    env, tr = make(pkg, n, T, max_steps=9, record_cap=cap)
+    tr.rollout()
+    torch.cuda.synchronize()
+    rew, done = tr.rew.cpu().numpy().reshape(T, n), tr.done.cpu().numpy().reshape(T, n).astype(bool)
+    rec = tr.episode_records()
+    assert rec.dropped == 0 and len(rec) == int(done.sum())
+    assert np.all(np.diff(rec.end_step) >= 0)
+    for i in range(n):
+        ends = np.nonzero(done[:, i])[0]
+        sel = rec.env_id == i
+        assert np.array_equal(rec.end_step[sel], ends)
+        starts = np.concatenate([[0], ends[:-1] + 1])
+        assert np.array_equal(rec.steps[sel], ends - starts + 1)
+        want = np.array([rew[s:e + 1, i].astype(np.float64).sum() for s, e in zip(starts, ends)])
+        np.testing.assert_allclose(rec.total_reward[sel], want, rtol=1e-5, atol=1e-6)
+    assert int(rec.success.sum()) == int(tr.ep_succ.sum().item())
+
+
+def test_curriculum_scheduler_hook(pkg):
+    """A progression decided on this iteration's records lands in the device curricula table."""
+    n, T = 64, 40
+    env, tr = make(pkg, n, T, max_steps=9, record_cap=8, success_rule="training")
+    C = pkg.CurriculumConfig
+    sched = pkg.experiments.CurriculumScheduler(C.easy(), C.hard(), success_rate_threshold=0.0,
+                                                min_episodes_before_progression=1, window_size=1,
+                                                progression_steps=4)
+    tr.attach_curriculum(sched)
+    tr.iteration()
+    torch.cuda.synchronize()
+    assert sched.total_episodes == int(tr.ep_count.sum().item()) > 0
+    assert sched.get_difficulty_level() == 1.0
+    cur = env.curriculum_configs[0]
+    assert float(cur.object_size) == float(sched.get_current_config().object_size)
+
+
+@pytest.mark.parametrize("std", [0.0, 0.05])
+def test_fused_observation_noise(pkg, std):
+    """Config C5: NoisyObservationWrapper (robustness_tests.py:140-171) fused into the rollout:
+    the policy sees obs + N(0, std^2) per element; the env state is untouched."""
+    n = 256
+    env, tr = make(pkg, n, 1, obs_noise_std=std)
+    clean = env.observe().clone()
+    jp0 = env.joint_positions.clone()
+    tr.rollout()
+    torch.cuda.synchronize()
+    seen = tr.obs_rm[:n, :45].float()
+    res = (seen - clean).cpu().numpy().ravel()
+    if std == 0.0:
+        np.testing.assert_array_equal(seen.cpu().numpy(), clean.to(torch.bfloat16).float().cpu().numpy())
+    else:
+        assert abs(res.mean()) < 3e-3 and 0.047 < res.std() < 0.053
+        # independent per element and per env
+        assert abs(np.corrcoef(res.reshape(n, 45)[:, 0], res.reshape(n, 45)[:, 1])[0, 1]) < 0.2
+    assert not torch.equal(env.joint_positions, jp0)  # the env stepped on its own state
+
+
+@pytest.mark.parametrize("std", [0.0, 0.05])
+def test_fused_dynamics_noise(pkg, std):
+    """Config C5: NoisyDynamicsWrapper (robustness_tests.py:174-211): the env integrates
+    clip(a + N(0, std^2), -1, 1) while the tape keeps the policy's action a.  The applied
+    action is recovered from the joint-velocity update jv' = 0.9 jv + 0.1 a (ME:203)."""
+    n = 256
+    env, tr = make(pkg, n, 1, dyn_noise_std=std)
+    jv0 = env.joint_velocities.clone().double()
+    tr.rollout()
+    torch.cuda.synchronize()
+    jv1 = env.joint_velocities.double()
+    applied = ((jv1 - np.float32(0.9) * jv0) / np.float32(0.1)).T.cpu().numpy()  # [n, 15]
+    policy = np.clip(tr.act[:n, :15].cpu().numpy(), -1, 1)
+    res = applied - policy
+    if std == 0.0:
+        assert np.abs(res).max() < 1e-4
+    else:
+        inner = res[(np.abs(applied) < 0.999) & (np.abs(policy) < 0.8)]
+        assert inner.size > 1000
+        assert abs(inner.mean()) < 4e-3 and 0.046 < inner.std() < 0.054

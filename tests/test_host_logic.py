@@ -144,3 +144,24 @@ def test_package_surface_imports_without_gpu():
     from dexterous_rl_manipulation_amd import envs
     with pytest.raises(Exception):
         envs.VecEnv(4)  # no GPU here: the product refuses to run (no CPU fallback)
+
+
+def test_scheduler_update_batch_equals_sequential_updates():
+    """CurriculumScheduler.update_batch (the trainer's per-iteration feed) == one update() per
+    episode (curriculum_scheduler.py:116-153): same lists, totals, progression points, history."""
+    from dexterous_rl_manipulation_amd.experiments import CurriculumConfig as CC, CurriculumScheduler
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        kw = dict(success_rate_threshold=float(rng.choice([0.0, 0.3, 0.5, 0.7])),
+                  min_episodes_before_progression=int(rng.integers(0, 40)), window_size=int(rng.integers(1, 25)),
+                  progression_steps=int(rng.integers(1, 7)))
+        a, b = CurriculumScheduler(CC.easy(), CC.hard(), **kw), CurriculumScheduler(CC.easy(), CC.hard(), **kw)
+        p = rng.random()
+        for _ in range(int(rng.integers(1, 6))):
+            m = int(rng.integers(0, 60))
+            s, st = rng.random(m) < p, rng.integers(1, 200, m)
+            assert any([a.update(bool(x), int(y)) for x, y in zip(s, st)]) == b.update_batch(s, st)
+            assert a.episode_successes == b.episode_successes and a.episode_steps == b.episode_steps
+            assert (a.total_steps, a.total_episodes) == (b.total_steps, b.total_episodes)
+            assert a.current_difficulty_level == b.current_difficulty_level
+            assert a.progression_history == b.progression_history and a.current_config == b.current_config

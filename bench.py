@@ -159,7 +159,7 @@ def pg_bench(args, world, rank, dev):
     wall = max_over_ranks(wall, world, dev)
     # phase breakdown (one extra iteration, outside the timed region)
     stream = torch.cuda.current_stream(dev)
-    names = ["rollout", "critic_forward", "advantages", "actor_forward", "heads", "backward", "optimizer_step"]
+    names = tr.phases()
     if tr.scheduler is not None:
         names.append("_feed_scheduler")  # records D2H + CurriculumScheduler.update_batch + table push
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
@@ -170,7 +170,8 @@ def pg_bench(args, world, rank, dev):
     torch.cuda.synchronize(dev)
     phases = {nm: round(evs[k].elapsed_time(evs[k + 1]), 4) for k, nm in enumerate(names)}
     M = tr.M
-    gemm_ms = phases["critic_forward"] + phases["actor_forward"] + phases["backward"]
+    gemm_ms = sum(v for k, v in phases.items() if k not in ("rollout", "advantages", "optimizer_step",
+                                                            "_feed_scheduler"))
     train_flops = M * (FWD_BOTH + BWD_BOTH)
     mfma = {"bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_BF16_TFS,
             "training_gemms_achieved": round(train_flops / (gemm_ms * 1e-3) / 1e12, 2),
@@ -181,7 +182,7 @@ def pg_bench(args, world, rank, dev):
     stats = tr.episode_stats()
     if tr.scheduler is not None:
         stats["curriculum_level"] = tr.scheduler.get_difficulty_level()
-        stats["scheduler_episodes"] = tr.scheduler.total_episodes
+        stats["scheduler_episodes"] = int(tr.scheduler.total_episodes)
     stats.update({k: round(v, 5) for k, v in tr.loss_stats().items()})
     return wall, phases, mfma, stats
 

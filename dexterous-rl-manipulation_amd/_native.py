@@ -87,6 +87,15 @@ class PgHeadsArgs(C.Structure):
                                           "grads")]
 
 
+class PgFusedArgs(C.Structure):
+    _fields_ = [("net", C.c_int32), ("train", C.c_int32), ("rows", C.c_int64)] + \
+               [(k, C.c_void_p) for k in ("packed", "params", "obs", "act", "logp_old", "adv", "ret", "stats")] + \
+               [(k, C.c_double) for k in ("inv_total_samples", "clip_eps", "vf_coef", "ent_coef")] + \
+               [(k, C.c_void_p) for k in ("values", "h1", "dh2", "partial", "loss_partial")] + \
+               [("grid", C.c_int32), ("wgrad_splits", C.c_int32), ("wgrad_partial", C.c_void_p),
+                ("grads", C.c_void_p)]
+
+
 _P = C.c_void_p
 _I32, _I64, _F64 = C.c_int32, C.c_int64, C.c_double
 _SIGS = {
@@ -117,6 +126,8 @@ _SIGS = {
     "dxrl_pg_adv_finalize": (C.c_int, [_I32, _I32, _P, _I64, _P, _P, _P]),
     "dxrl_pg_heads": (C.c_int, [_I32, C.POINTER(PgHeadsArgs), _P]),
     "dxrl_pg_grad_sumsq": (C.c_int, [_I32, _P, _I64, _P, _P, _P]),
+    "dxrl_pg_fused_sizes": (C.c_int, [C.POINTER(_I32), C.POINTER(_I64)]),
+    "dxrl_pg_fused": (C.c_int, [_I32, C.POINTER(PgFusedArgs), _P]),
     "dxrl_pg_adam": (C.c_int, [_I32, _P, _P, _P, _P, _I64, _F64, _F64, _F64, _F64, _I64, _P, _F64, _P]),
 }
 

@@ -18,19 +18,8 @@ using namespace dxrl;
 
 namespace dxrl {
 
-typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-typedef __attribute__((address_space(3))) bf16 lds_bf16;
-
 constexpr int kBM = 128, kBN = 128, kBK = 64;
 constexpr int kAPitch = kBK + 8;  // 144-B rows: conflict-free ds_read_b128 fragment reads
-
-__device__ __forceinline__ bf16x8 zero8() {
-    bf16x8 z;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) z[j] = (bf16)0.0f;
-    return z;
-}
 
 // ------------------------------------------------------------------ C = A . Bt^T
 __global__ __launch_bounds__(256) void k_gemm_bf16(GemmArgs g) {
@@ -257,22 +246,6 @@ static bool panel_ok(const GemmArgs& g, int splits) {
 // 16-lane group g) then touch all 64 banks once per 32-lane half.
 constexpr int kWO = 128, kWI = 128, kWK = 64, kWPitch = 128 + 32;
 
-__device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int col0, int kk, int lane) {
-    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const int row = kk + 8 * (g >> 1) + q;
-    const int col = col0 + 16 * (g & 1) + 4 * p;
-    lds_bf16* base = (lds_bf16*)(tile);  // generic -> LDS address space (the tile is __shared__)
-    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + row * kWPitch + col));
-    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + (row + 4) * kWPitch + col));
-    bf16x8 v;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        v[j] = lo[j];
-        v[4 + j] = hi[j];
-    }
-    return v;
-}
-
 struct WgradArgs {
     const bf16* Y;  // [M][ldy], O used columns
     int64_t ldy;
@@ -331,9 +304,9 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16(WgradArgs w) {
         for (int kk = 0; kk < kWK; kk += 16) {
             bf16x8 a[2], b[2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) a[i] = tr_frag(Ys, wo + 32 * i, kk, lane);
+            for (int i = 0; i < 2; ++i) a[i] = tr_frag<kWPitch>(Ys, wo + 32 * i, kk, lane);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) b[j] = tr_frag(Xs, wi + 32 * j, kk, lane);
+            for (int j = 0; j < 2; ++j) b[j] = tr_frag<kWPitch>(Xs, wi + 32 * j, kk, lane);
             if (wave_live) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i)

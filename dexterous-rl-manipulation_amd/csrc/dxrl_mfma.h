@@ -15,6 +15,16 @@ namespace dxrl {
 typedef __bf16 bf16;
 typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef __attribute__((address_space(3))) bf16 lds_bf16;
+
+__device__ __forceinline__ bf16x8 zero8() {
+    bf16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = (bf16)0.0f;
+    return z;
+}
 
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -32,6 +42,26 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16* base, int64_t ld, int64_
 #pragma unroll
     for (int j = 0; j < 8; ++j) z[j] = (bf16)0.0f;
     return z;
+}
+
+// k-major MFMA fragment from a row-major [k][feature] LDS tile (ds_read_b64_tr_b16): lane l
+// gets T[kk + 8h + j][col0 + (l & 31)], j = 0..7 -- i.e. the operand row "feature col0 + r"
+// over the 16 k values kk..kk+15.  Every lane must execute it (EXEC all ones).
+template <int kPitch>
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int col0, int kk, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int row = kk + 8 * (g >> 1) + q;
+    const int col = col0 + 16 * (g & 1) + 4 * p;
+    lds_bf16* base = (lds_bf16*)(tile);  // generic -> LDS address space (the tile is __shared__)
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + row * kPitch + col));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + (row + 4) * kPitch + col));
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = lo[j];
+        v[4 + j] = hi[j];
+    }
+    return v;
 }
 
 __device__ __forceinline__ float tanh_f(float x) {

@@ -1,0 +1,543 @@
+// dxrl_pg_fused.hip -- one-pass training step of one MLP(256,256) head network.
+//
+// k_pg_fused runs, per 128-sample tile and entirely out of LDS (160 KiB, one
+// workgroup of 8 waves per CU, persistent over tiles):
+//
+//   forward   H1 = tanh(X W1^T)  H2 = tanh(H1 W2^T + b2)  out = H2 W3^T + b3
+//   heads     actor: PPO-clip surrogate -> dL/dmu, dL/dlog_std, losses
+//             critic: value loss -> dL/dV            (forward mode: write V)
+//   backward  dW3 += dout^T H2            (registers, whole launch)
+//             dH2 = (dout W3) * (1 - H2^2)            -> HBM (for dW2)
+//             dH1 = (dH2 W2) * (1 - H1^2)
+//             dW1 += dH1^T X              (registers, whole launch)
+//
+// H1 and dH2 go to HBM once so the one contraction too large to keep in
+// registers, dW2 = dH2^T [H1 | 1], runs as the split-K weight-gradient GEMM
+// (launch_wgrad) right after.  Nothing else of the activations ever leaves
+// the CU: compared with the layer-by-layer GEMM chain this removes the H2,
+// dH1, mu / dout round trips and five of the eight launches.
+//
+// MFMA formulation: hidden layers are computed transposed (weights as the A
+// operand from L2, activations as the B operand from LDS), so each lane's
+// accumulator holds 4 consecutive features of one sample -> 8-byte LDS stores
+// of the row-major activation tile.  Transposed operands of the weight
+// gradients come straight from the row-major tiles through ds_read_b64_tr_b16.
+//
+// Gradients are deterministic: each workgroup owns a fixed tile set and writes
+// its dW1 / dW3 / dlog_std partials once; k_fused_reduce sums them in block order.
+#include "dxrl_gemm.h"
+#include "dxrl_pg.h"
+
+using namespace dxrl;
+using namespace dxrl::pg;
+
+namespace dxrl {
+namespace {
+
+constexpr float kLog2PiF = 1.8378770664093453f;
+constexpr int kTR = 128;                 // samples per tile
+constexpr int kFW = 4;                   // waves per workgroup: one per SIMD, 512 registers each
+constexpr int kFThreads = 64 * kFW;
+constexpr int kNT = kH / 32 / kFW;       // 32-wide feature tiles per wave (2)
+constexpr int kXp = kIn + 8;             // 72:  X rows (conflict-free b128 row reads)
+constexpr int kHp = kH + 8;              // 264: H1 / H2 rows
+constexpr int kDp = kOut + 8;            // 40:  dout rows
+constexpr int kOffX = 0;
+constexpr int kOffH1 = kOffX + kTR * kXp;
+constexpr int kOffH2 = kOffH1 + kTR * kHp;
+constexpr int kOffD = kOffH2 + kTR * kHp;
+constexpr int kLdsElems = kOffD + kTR * kDp;
+static_assert(kLdsElems * 2 == 163840, "the fused kernel uses exactly the CU's 160 KiB of LDS");
+static_assert(kTR / 32 == kFW, "one 32-sample head tile per wave");
+
+// per-workgroup gradient partial slab (f32)
+constexpr int kPartW1 = 0;                   // [256][64]
+constexpr int kPartW3 = kPartW1 + kH * kIn;  // [32][288]
+constexpr int kPartLs = kPartW3 + kOut * kHx;
+constexpr int kPartSize = kPartLs + 16;
+
+struct FusedArgs {
+    int net;    // 0 actor, 1 critic
+    int train;  // 0: forward only (critic values), 1: forward + heads + backward
+    int64_t rows;
+    const bf16* X;  // [rows][64], column 45 = 1
+    const bf16 *W1, *W2, *W3, *W2T, *W3T;
+    const float* b2;  // bias of hidden unit n: b2[n * kHx]
+    const float* b3;  // bias of head row o:   b3[o * kHx]
+    const float* logstd;
+    const float* act;
+    const float* logp_old;
+    const float* adv;
+    const float* ret;
+    const double* stats;
+    float sc, clip_eps, vf2;
+    float* v_out;   // forward mode: [rows]
+    bf16* h1_out;   // [rows][kHx] (columns 0..255 written)
+    bf16* dh2_out;  // [rows][kH]
+    float* part;    // [grid][kPartSize]
+    double* loss;   // [grid][4]
+};
+
+__device__ __forceinline__ void zero_acc(f32x16& a) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a[q] = 0.0f;
+}
+
+// acc[j][mt] (features 32 (ft0 + j).. x samples 32 mt..) = W[32 (ft0 + j) + r][:] . A[32 mt + r][:]
+// over KS k-steps.  Weight fragments stream from L2 one 4-k-step chunk ahead (double
+// buffer); each activation fragment read from LDS feeds NT MFMAs.
+template <int KS, int kLda, int NT>
+__device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int ldw, int ft0, const bf16* A,
+                                          f32x16 (&acc)[NT][4], int lane) {
+    const int r = lane & 31, h = lane >> 5;
+    constexpr int kC = KS < 4 ? KS : 4;  // k-steps per chunk
+    static_assert(KS % kC == 0, "chunking");
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) zero_acc(acc[j][mt]);
+    const bf16* wp[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) wp[j] = W + (int64_t)(32 * (ft0 + j) + r) * ldw + 8 * h;
+    bf16x8 cur[kC][NT], nxt[kC][NT];
+#pragma unroll
+    for (int k = 0; k < kC; ++k)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) cur[k][j] = *reinterpret_cast<const bf16x8*>(wp[j] + 16 * k);
+#pragma unroll 1
+    for (int kc = 0; kc < KS; kc += kC) {
+        if (kc + kC < KS) {
+#pragma unroll
+            for (int k = 0; k < kC; ++k)
+#pragma unroll
+                for (int j = 0; j < NT; ++j) nxt[k][j] = *reinterpret_cast<const bf16x8*>(wp[j] + 16 * (kc + kC + k));
+        }
+#pragma unroll
+        for (int k = 0; k < kC; ++k)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(A + (32 * mt + r) * kLda + 16 * (kc + k) + 8 * h);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[j][mt] = mfma32(cur[k][j], b, acc[j][mt]);
+            }
+#pragma unroll
+        for (int k = 0; k < kC; ++k)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) cur[k][j] = nxt[k][j];
+    }
+}
+
+// tanh(acc + bias) -> bf16 row-major activation tile (4 consecutive features per 8-byte store)
+__device__ __forceinline__ void store_hidden(const f32x16 (&acc)[1][4], int ft, const float* __restrict__ bias,
+                                             bf16* H, int lane) {
+    const int r = lane & 31, h = lane >> 5;
+    constexpr int j = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f0 = 32 * ft + 8 * g + 4 * h;
+            float b[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (bias) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) b[u] = bias[(int64_t)(f0 + u) * kHx];
+            }
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                bf16x4 v;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = to_bf16(tanh_f(acc[j][mt][4 * g + u] + b[u]));
+                *reinterpret_cast<bf16x4*>(H + (32 * mt + r) * kHp + f0) = v;
+            }
+        }
+}
+
+// Y[m][f] <- bf16(acc[f][m] * (1 - Y[m][f]^2)) for this wave's features (tanh' gate, in place)
+__device__ __forceinline__ void gate_in_place(const f32x16 (&acc)[1][4], int ft, bf16* Y, int lane) {
+    const int r = lane & 31, h = lane >> 5;
+    constexpr int j = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f0 = 32 * ft + 8 * g + 4 * h;
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                bf16x4* yp = reinterpret_cast<bf16x4*>(Y + (32 * mt + r) * kHp + f0);
+                const bf16x4 y = *yp;
+                bf16x4 v;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float yy = from_bf16(y[u]);
+                    v[u] = to_bf16(acc[j][mt][4 * g + u] * (1.0f - yy * yy));
+                }
+                *yp = v;
+            }
+        }
+}
+
+__global__ __launch_bounds__(kFThreads, 1) void k_pg_fused(FusedArgs p) {
+    __shared__ __attribute__((aligned(16))) bf16 lds[kLdsElems];
+    bf16* X = lds + kOffX;
+    bf16* H1 = lds + kOffH1;
+    bf16* H2 = lds + kOffH2;
+    bf16* D = lds + kOffD;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int ft0 = kNT * wave;  // this wave's first 32-wide feature tile
+    const int64_t ntiles = (p.rows + kTR - 1) / kTR;
+
+    // launch-long accumulators: dW3 columns of this wave's tiles, dW1 rows of this wave's tiles
+    f32x16 acc3[kNT], acc1[kNT][2];
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+        zero_acc(acc3[j]);
+        zero_acc(acc1[j][0]);
+        zero_acc(acc1[j][1]);
+    }
+    float dls[8], db3[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dls[j] = db3[j] = 0.0f;
+    double lsum[4] = {0.0, 0.0, 0.0, 0.0};
+
+    const double adv_mean = p.train && p.net == 0 ? p.stats[2] : 0.0;
+    const double adv_div = p.train && p.net == 0 ? p.stats[4] + 1e-8 : 1.0;
+
+    // X tile prefetch: 128 rows x 8 chunks of 16 B = 1024 chunks, 4 per thread
+    constexpr int kXU = kTR * (kIn / 8) / kFThreads;
+    bf16x8 xr[kXU];
+    auto fetch_x = [&](int64_t tile) {
+#pragma unroll
+        for (int u = 0; u < kXU; ++u) {
+            const int c = tid + kFThreads * u, row = c >> 3, col = 8 * (c & 7);
+            const int64_t m = tile * kTR + row;
+            xr[u] = m < p.rows ? *reinterpret_cast<const bf16x8*>(p.X + m * kIn + col) : zero8();
+        }
+    };
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) fetch_x(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t m0 = tile * kTR;
+#pragma unroll
+        for (int u = 0; u < kXU; ++u) {
+            const int c = tid + kFThreads * u, row = c >> 3, col = 8 * (c & 7);
+            *reinterpret_cast<bf16x8*>(X + row * kXp + col) = xr[u];
+        }
+        __syncthreads();
+        if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
+
+        // ---- L1, L2 (wave w: hidden features 64w .. 64w + 63, all 128 samples)
+#pragma unroll 1
+        for (int j = 0; j < kNT; ++j) {
+            f32x16 acc[1][4];
+            fwd_tiles<kIn / 16, kXp, 1>(p.W1, kIn, ft0 + j, X, acc, lane);  // bias = W1 column 45 (X column 45 = 1)
+            store_hidden(acc, ft0 + j, nullptr, H1, lane);
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int j = 0; j < kNT; ++j) {
+            f32x16 acc[1][4];
+            fwd_tiles<kH / 16, kHp, 1>(p.W2, kHx, ft0 + j, H1, acc, lane);
+            store_hidden(acc, ft0 + j, p.b2, H2, lane);
+        }
+        __syncthreads();
+
+        // ---- head: wave w owns samples 32w .. 32w + 31 (lane: sample r, head rows of half h)
+        {
+            f32x16 acc;
+            zero_acc(acc);
+            const bf16* wrow = p.W3 + (int64_t)r * kHx + 8 * h;
+#pragma unroll
+            for (int k = 0; k < kH / 16; ++k) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + 16 * k);
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * k + 8 * h);
+                acc = mfma32(a, b, acc);
+            }
+            const int ml = 32 * wave + r;
+            const int64_t m = m0 + ml;
+            const bool valid = m < p.rows;
+            float d[8], b3v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                d[q] = 0.0f;
+                b3v[q] = p.b3[(int64_t)((q & 3) + 8 * (q >> 2) + 4 * h) * kHx];  // head row o of register q
+            }
+            if (p.net == 0) {
+                if (p.train) {
+                    float mu[8], a[8], lsv[8], iv2[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int o = (q & 3) + 8 * (q >> 2) + 4 * h;
+                        lsv[q] = o < kAct ? p.logstd[o] : 0.0f;
+                        iv2[q] = __expf(-2.0f * lsv[q]);
+                    }
+                    float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+                    float lo = 0.0f, adv = 0.0f;
+                    if (valid) {
+                        a0 = *reinterpret_cast<const float4*>(p.act + m * kActPad + 4 * h);
+                        a1 = *reinterpret_cast<const float4*>(p.act + m * kActPad + 8 + 4 * h);
+                        lo = p.logp_old[m];
+                        adv = p.adv[m];
+                    }
+                    a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w;
+                    a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
+                    // log pi(a|s): the 15 terms summed in action order (as the rollout sampled
+                    // them), so the first update's ratios are exactly 1
+                    float t[8], u[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int o = (q & 3) + 8 * (q >> 2) + 4 * h;
+                        mu[q] = acc[q] + b3v[q];
+                        const float z = (a[q] - mu[q]) * __expf(-lsv[q]);
+                        t[q] = o < kAct ? -0.5f * z * z - lsv[q] - 0.5f * kLog2PiF : 0.0f;
+                    }
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) u[q] = __shfl_xor(t[q], 32);
+                    float lp = 0.0f;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) lp += h ? u[q] : t[q];      // o = 0..3
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) lp += h ? t[q] : u[q];      // o = 4..7
+#pragma unroll
+                    for (int q = 4; q < 8; ++q) lp += h ? u[q] : t[q];      // o = 8..11
+#pragma unroll
+                    for (int q = 4; q < 7; ++q) lp += h ? t[q] : u[q];      // o = 12..14
+                    const float ratio = __expf(lp - lo);
+                    const float A = (float)(((double)adv - adv_mean) / adv_div);
+                    const float s1 = ratio * A;
+                    const float rc = fminf(fmaxf(ratio, 1.0f - p.clip_eps), 1.0f + p.clip_eps);
+                    const float s2 = rc * A;
+                    float g = 0.0f;
+                    if (s1 <= s2 || ratio == rc) g = -A * ratio;  // d(-min(s1, s2)) / d logp
+                    g *= p.sc;
+                    if (valid) {
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) {
+                            const int o = (q & 3) + 8 * (q >> 2) + 4 * h;
+                            if (o < kAct) {
+                                const float dd = a[q] - mu[q];
+                                d[q] = from_bf16(to_bf16(g * dd * iv2[q]));  // dlogp/dmu = (a - mu) / sigma^2
+                                dls[q] += g * (dd * dd * iv2[q] - 1.0f);       // dlogp/dlogstd
+                                db3[q] += d[q];
+                            }
+                        }
+                        if (h == 0) {
+                            lsum[0] += -(double)fminf(s1, s2);
+                            lsum[2] += fabsf(ratio - 1.0f) > p.clip_eps ? 1.0 : 0.0;
+                            lsum[3] += (double)(lo - lp);
+                        }
+                    }
+                }
+            } else {
+                const float v = acc[0] + b3v[0];  // lanes h == 0 hold head row 0
+                if (!p.train) {
+                    if (valid && h == 0) p.v_out[m] = v;
+                } else if (valid && h == 0) {
+                    const float e = v - p.ret[m];
+                    d[0] = from_bf16(to_bf16(p.vf2 * e * p.sc));
+                    db3[0] += d[0];
+                    lsum[1] += (double)e * (double)e;
+                }
+            }
+            if (p.train) {
+#pragma unroll
+                for (int g2 = 0; g2 < 4; ++g2) {  // head rows 8 g2 + 4 h .. + 3
+                    bf16x4 v;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] = g2 < 2 ? to_bf16(d[4 * g2 + u]) : (bf16)0.0f;
+                    *reinterpret_cast<bf16x4*>(D + ml * kDp + 8 * g2 + 4 * h) = v;
+                }
+            }
+        }
+        if (!p.train) {
+            __syncthreads();  // X / H1 / H2 are rewritten by the next tile
+            continue;
+        }
+        // H1 tile -> HBM (B operand of the dW2 GEMM): 128 rows x 32 chunks of 16 B
+#pragma unroll 4
+        for (int c = tid; c < kTR * (kH / 8); c += kFThreads) {
+            const int row = c >> 5, col = 8 * (c & 31);
+            const int64_t m = m0 + row;
+            if (m < p.rows)
+                *reinterpret_cast<bf16x8*>(p.h1_out + m * kHx + col) = *reinterpret_cast<const bf16x8*>(H1 + row * kHp + col);
+        }
+        __syncthreads();
+
+        // ---- dW3 += dout^T H2 (wave w: H2 columns of its tiles), then dH2 in place of H2
+#pragma unroll
+        for (int kk = 0; kk < kTR; kk += 16) {
+            const bf16x8 a = tr_frag<kDp>(D, 0, kk, lane);
+#pragma unroll
+            for (int j = 0; j < kNT; ++j) acc3[j] = mfma32(a, tr_frag<kHp>(H2, 32 * (ft0 + j), kk, lane), acc3[j]);
+        }
+#pragma unroll 1
+        for (int j = 0; j < kNT; ++j) {
+            f32x16 acc[1][4];
+            fwd_tiles<kOut / 16, kDp, 1>(p.W3T, kOut, ft0 + j, D, acc, lane);  // dH2^T = W3^T dout^T
+            gate_in_place(acc, ft0 + j, H2, lane);
+        }
+        __syncthreads();
+
+        // ---- dH2 -> HBM; dH1 = (dH2 W2) * (1 - H1^2)  (wave w: L2 inputs of its tiles, rows = samples)
+#pragma unroll 4
+        for (int c = tid; c < kTR * (kH / 8); c += kFThreads) {
+            const int row = c >> 5, col = 8 * (c & 31);
+            const int64_t m = m0 + row;
+            if (m < p.rows)
+                *reinterpret_cast<bf16x8*>(p.dh2_out + m * kH + col) = *reinterpret_cast<const bf16x8*>(H2 + row * kHp + col);
+        }
+#pragma unroll 1
+        for (int j = 0; j < kNT; ++j) {
+            f32x16 acc[1][4];
+            fwd_tiles<kH / 16, kHp, 1>(p.W2T, kH, ft0 + j, H2, acc, lane);  // dH1^T = W2^T dH2^T
+            gate_in_place(acc, ft0 + j, H1, lane);                             // H1 is in HBM already
+        }
+        __syncthreads();
+
+        // ---- dW1 += dH1^T X (wave w: hidden rows of its tiles, input columns 0..63)
+#pragma unroll
+        for (int kk = 0; kk < kTR; kk += 16) {
+            bf16x8 b[2];
+#pragma unroll
+            for (int it = 0; it < 2; ++it) b[it] = tr_frag<kXp>(X, 32 * it, kk, lane);
+#pragma unroll
+            for (int j = 0; j < kNT; ++j) {
+                const bf16x8 a = tr_frag<kHp>(H1, 32 * (ft0 + j), kk, lane);
+#pragma unroll
+                for (int it = 0; it < 2; ++it) acc1[j][it] = mfma32(a, b[it], acc1[j][it]);
+            }
+        }
+        __syncthreads();
+    }
+    if (!p.train) return;
+
+    // ---- workgroup partials (fixed layout; reduced in block order by k_fused_reduce)
+    float* part = p.part + (int64_t)blockIdx.x * kPartSize;
+#pragma unroll
+    for (int j = 0; j < kNT; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int o = acc_row(q, lane);
+            part[kPartW3 + o * kHx + 32 * (ft0 + j) + r] = acc3[j][q];
+#pragma unroll
+            for (int it = 0; it < 2; ++it) part[kPartW1 + (32 * (ft0 + j) + o) * kIn + 32 * it + r] = acc1[j][it][q];
+        }
+    float* red = reinterpret_cast<float*>(lds);              // [256 lanes][16]
+    double* lred = reinterpret_cast<double*>(lds + kOffH1);  // [256 lanes][4]
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        red[tid * 16 + q] = dls[q];
+        red[tid * 16 + 8 + q] = db3[q];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lred[tid * 4 + k] = lsum[k];
+    __syncthreads();
+    if (tid < 32) {  // head row o: lanes with h = (o >> 2) & 1, register q = (o & 3) + 4 (o >> 3)
+        const int o = tid, hh = (o >> 2) & 1, q = (o & 3) + 4 * (o >> 3);
+        float sl = 0.0f, sb = 0.0f;
+        if (o < 16) {
+            for (int w = 0; w < kFW; ++w)
+                for (int rr = 0; rr < 32; ++rr) {
+                    const int t = 64 * w + 32 * hh + rr;
+                    sl += red[t * 16 + q];
+                    sb += red[t * 16 + 8 + q];
+                }
+        }
+        part[kPartW3 + o * kHx + kH] = sb;  // bias column of the head
+        if (o < 16) part[kPartLs + o] = sl;
+    } else if (tid < 36) {
+        const int k = tid - 32;
+        double s = 0.0;
+        for (int t = 0; t < kFThreads; ++t) s += lred[t * 4 + k];
+        if ((p.net == 0) == (k != 1)) p.loss[(int64_t)blockIdx.x * 4 + k] = s;
+    }
+}
+
+// grads blocks W1 / W3 (and log_std for the actor) = sum over workgroups, fixed order
+__global__ void k_fused_reduce(const float* __restrict__ part, int nb, float* __restrict__ gW1, float* __restrict__ gW3,
+                               float* __restrict__ gLs, float ent_coef) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= kPartSize) return;
+    const int col = (j - kPartW3) % kHx;
+    const bool w3pad = j >= kPartW3 && j < kPartLs && col > kH;  // never written
+    float s = 0.0f;
+    if (!w3pad)
+        for (int b = 0; b < nb; ++b) s += part[(int64_t)b * kPartSize + j];
+    if (j < kPartW3) gW1[j] = s;
+    else if (j < kPartLs) gW3[j - kPartW3] = s;
+    else if (gLs) {
+        const int k = j - kPartLs;
+        gLs[k] = k < kAct ? s - ent_coef : 0.0f;
+    }
+}
+
+}  // namespace
+}  // namespace dxrl
+
+// =========================================================================== C ABI
+extern "C" {
+
+int dxrl_pg_fused_sizes(int32_t* tile_rows, int64_t* partial_floats_per_block) {
+    DXRL_REQUIRE(tile_rows && partial_floats_per_block, "null outputs");
+    *tile_rows = kTR;
+    *partial_floats_per_block = kPartSize;
+    return DXRL_OK;
+}
+
+int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
+    DXRL_REQUIRE(a && a->packed && a->params && a->obs && a->rows > 0, "fused: null arguments");
+    DXRL_REQUIRE(a->net == 0 || a->net == 1, "fused: net must be 0 (actor) or 1 (critic)");
+    DXRL_REQUIRE(a->grid >= 1 && a->grid <= 65535, "fused: grid out of range");
+    const bool train = a->train != 0;
+    if (!train) DXRL_REQUIRE(a->net == 1 && a->values, "fused: forward mode computes critic values only");
+    if (train) {
+        DXRL_REQUIRE(a->h1 && a->dh2 && a->partial && a->loss_partial && a->grads && a->wgrad_partial &&
+                         a->wgrad_splits >= 1,
+                     "fused: training needs h1/dh2 scratch, partial slabs and grads");
+        DXRL_REQUIRE(a->net == 1 ? (a->ret != nullptr) : (a->act && a->logp_old && a->adv && a->stats),
+                     "fused: missing head inputs");
+        DXRL_REQUIRE((reinterpret_cast<uintptr_t>(a->act) & 15) == 0, "fused: act must be 16-byte aligned");
+    }
+    DXRL_REQUIRE((reinterpret_cast<uintptr_t>(a->obs) & 15) == 0, "fused: obs must be 16-byte aligned");
+    DeviceGuard g(device);
+    hipStream_t st = as_stream(stream);
+    const bf16* w = static_cast<const bf16*>(a->packed);
+    const bool c = a->net == 1;
+    const int64_t o2 = c ? kOffW2c : kOffW2a, o3 = c ? kOffW3c : kOffW3a;
+    FusedArgs f{};
+    f.net = a->net;
+    f.train = train;
+    f.rows = a->rows;
+    f.X = static_cast<const bf16*>(a->obs);
+    f.W1 = w + (c ? kBfW1c : kBfW1a);
+    f.W2 = w + (c ? kBfW2c : kBfW2a);
+    f.W3 = w + (c ? kBfW3c : kBfW3a);
+    f.W2T = w + (c ? kBfW2cT : kBfW2aT);
+    f.W3T = w + (c ? kBfW3cT : kBfW3aT);
+    f.b2 = a->params + o2 + kH;
+    f.b3 = a->params + o3 + kH;
+    f.logstd = a->params + kOffLogStd;
+    f.act = a->act;
+    f.logp_old = a->logp_old;
+    f.adv = a->adv;
+    f.ret = a->ret;
+    f.stats = a->stats;
+    f.sc = (float)a->inv_total_samples;
+    f.clip_eps = (float)a->clip_eps;
+    f.vf2 = (float)(2.0 * a->vf_coef);
+    f.v_out = a->values;
+    f.h1_out = static_cast<bf16*>(a->h1);
+    f.dh2_out = static_cast<bf16*>(a->dh2);
+    f.part = a->partial;
+    f.loss = a->loss_partial;
+    const int64_t ntiles = (a->rows + kTR - 1) / kTR;
+    const int grid = (int)(ntiles < a->grid ? ntiles : a->grid);
+    hipLaunchKernelGGL(k_pg_fused, dim3(grid), dim3(kFThreads), 0, st, f);
+    if (int rc = launch_check("k_pg_fused")) return rc;
+    if (!train) return DXRL_OK;
+    float* G = a->grads;
+    hipLaunchKernelGGL(k_fused_reduce, dim3((kPartSize + 255) / 256), dim3(256), 0, st, a->partial, grid,
+                       G + (c ? kOffW1c : kOffW1a), G + o3, c ? nullptr : G + kOffLogStd, (float)a->ent_coef);
+    if (int rc = launch_check("k_fused_reduce")) return rc;
+    // dW2 = dH2^T [H1 | 1]: bias gradient lands in column 256
+    return launch_wgrad(static_cast<const bf16*>(a->dh2), kH, kH, static_cast<const bf16*>(a->h1), kHx, kHx, a->rows,
+                        a->wgrad_splits, a->wgrad_partial, G + o2, st);
+}
+
+}  // extern "C"

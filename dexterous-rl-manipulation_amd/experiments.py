@@ -217,13 +217,13 @@ class CurriculumScheduler:
             self.episode_successes.extend(s[done:j + 1].tolist())
             self.episode_steps.extend(st[done:j + 1].tolist())
             self.total_steps += int(steps_cum[j] - (steps_cum[done - 1] if done else 0))
-            self.total_episodes += j + 1 - done
-            done = j + 1
+            self.total_episodes += int(j + 1 - done)
+            done = int(j + 1)
             progressed |= self._progress()
         self.episode_successes.extend(s[done:].tolist())
         self.episode_steps.extend(st[done:].tolist())
         self.total_steps += int(steps_cum[-1] - (steps_cum[done - 1] if done else 0))
-        self.total_episodes += n - done
+        self.total_episodes += int(n - done)
         return progressed
 
     def _window_rate(self):

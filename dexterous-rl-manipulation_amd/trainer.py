@@ -71,6 +71,7 @@ class TrainerConfig:
     dyn_noise_std: float = 0.0               # config C5: 0.05
     seed: int = 0
     splitk_target_blocks: int = 768
+    fused: bool = True                       # one-pass learner kernels (dxrl_pg_fused) vs the GEMM chain
     record_cap: int = 0                      # per-env episode records per iteration (0 = off)
     success_rule: str = "terminated"         # "training" (episode_utils.py:52) or "terminated"
 
@@ -138,6 +139,11 @@ class PGTrainer:
         self.splits = max(1, min(cfg.splitk_target_blocks // 6, M // 4096))
         self.kpartial = z(self.splits, H, HX)
         self.gnorm2 = torch.zeros(1, dtype=torch.float64, device=d)
+        tr_, pf_ = C.c_int32(), C.c_int64()
+        N.call("dxrl_pg_fused_sizes", C.byref(tr_), C.byref(pf_))
+        self.fused_grid = int(torch.cuda.get_device_properties(d).multi_processor_count)
+        self.fused_partial = z(self.fused_grid, pf_.value)
+        self.fused_loss = torch.zeros(self.fused_grid, 4, dtype=torch.float64, device=d)
         self.pack()
 
     # ------------------------------------------------------------------ params
@@ -214,6 +220,37 @@ class PGTrainer:
     def actor_forward(self):
         self._mlp_forward("a", self.M, self.H1a, self.H2a, head_f32=self.mu)
 
+    # ------------------------------------------------------------------ fused path
+    def _fused_args(self, net, train, rows):
+        c, p = self.cfg, N.ptr
+        f = N.PgFusedArgs()
+        f.net, f.train, f.rows = net, int(train), rows
+        f.packed, f.params, f.obs = p(self.packed), p(self.params), p(self.obs_rm)
+        f.act, f.logp_old, f.adv, f.ret, f.stats = p(self.act), p(self.logp), p(self.adv), p(self.ret), p(self.stats)
+        f.inv_total_samples = 1.0 / (self.M * self.world)
+        f.clip_eps, f.vf_coef, f.ent_coef = c.clip_eps, c.vf_coef, c.ent_coef / self.world
+        f.values = p(self.V[0])
+        f.h1, f.dh2 = p(self.H1a), p(self.dH2)
+        f.partial, f.loss_partial, f.grid = p(self.fused_partial), p(self.fused_loss), self.fused_grid
+        f.wgrad_splits, f.wgrad_partial, f.grads = self.splits, p(self.kpartial), p(self.grads)
+        return f
+
+    def critic_values(self):
+        """V over the T + 1 observation blocks (fused forward, nothing stored but V)."""
+        N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(1, False, self.M + self.n)), self._s())
+
+    def actor_train(self):
+        N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(0, True, self.M)), self._s())
+
+    def critic_train(self):
+        N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(1, True, self.M)), self._s())
+
+    def phases(self):
+        """The iteration's launch groups in order (bench.py times each)."""
+        if self.cfg.fused:
+            return ["rollout", "critic_values", "advantages", "actor_train", "critic_train", "optimizer_step"]
+        return ["rollout", "critic_forward", "advantages", "actor_forward", "heads", "backward", "optimizer_step"]
+
     def _allreduce(self, t):
         all_reduce_sum_(t, self.world, self.pg)
 
@@ -283,14 +320,9 @@ class PGTrainer:
         return rec
 
     def iteration(self, update: bool = True):
-        self.rollout()
-        self.critic_forward()
-        self.advantages()
-        self.actor_forward()
-        self.heads()
-        self.backward()
-        if update:
-            self.optimizer_step()
+        for name in self.phases():
+            if name != "optimizer_step" or update:
+                getattr(self, name)()
         if self.scheduler is not None:
             self._feed_scheduler()
         self.iteration_index += 1
@@ -306,6 +338,6 @@ class PGTrainer:
         return out
 
     def loss_stats(self) -> Dict[str, float]:
-        s = self.loss_partial.sum(0).cpu().numpy() / self.M
+        s = (self.fused_loss if self.cfg.fused else self.loss_partial).sum(0).cpu().numpy() / self.M
         return {"policy_loss": float(s[0]), "value_mse": float(s[1]), "clip_frac": float(s[2]),
                 "approx_kl": float(s[3]), "grad_norm": float(np.sqrt(self.gnorm2.item()))}

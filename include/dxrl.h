@@ -292,6 +292,40 @@ int dxrl_pg_adam(int32_t device, float* params, const float* grads, float* m1, f
                  double beta1, double beta2, double eps, int64_t step, const double* gnorm2, double max_norm,
                  void* stream);
 
+/* ---- fused one-pass learner step (csrc/dxrl_pg_fused.hip) ----------------------------
+ * One launch per network replaces forward GEMMs + heads + backward GEMMs of the
+ * layer-by-layer path (dxrl_gemm_bf16 / dxrl_pg_heads / dxrl_wgrad_bf16): per
+ * 128-sample tile it runs the MLP forward, the PPO-clip (actor) or value (critic)
+ * head and the backward pass out of LDS, then dW2 = dH2^T [H1 | 1] by split-K.
+ * train == 0 (critic only): forward pass writing values[rows] (GAE bootstrap pass). */
+typedef struct dxrl_pg_fused_args {
+    int32_t net;               /* 0 actor, 1 critic                                        */
+    int32_t train;             /* 0 forward only (critic values), 1 forward + backward     */
+    int64_t rows;              /* samples                                                  */
+    const void* packed;        /* bf16 weight pack (dxrl_pg_pack_weights)                  */
+    const float* params;       /* f32 master parameters (biases, log_std)                  */
+    const void* obs;           /* bf16 [rows][64], column 45 = 1                           */
+    const float* act;          /* actor: f32 [rows][16]                                    */
+    const float* logp_old;     /* actor: f32 [rows]                                        */
+    const float* adv;          /* actor: f32 [rows] raw GAE advantages                     */
+    const float* ret;          /* critic: f32 [rows] returns                               */
+    const double* stats;       /* actor: normalisation stats (mean [2], std [4])           */
+    double inv_total_samples;  /* 1 / (samples summed over ranks)                          */
+    double clip_eps, vf_coef, ent_coef;
+    float* values;             /* forward mode: f32 [rows]                                 */
+    void* h1;                  /* bf16 [rows][288] scratch, column 256 preset to 1         */
+    void* dh2;                 /* bf16 [rows][256] scratch                                 */
+    float* partial;            /* f32 [grid][dxrl_pg_fused_sizes().partial_floats]         */
+    double* loss_partial;      /* f64 [grid][4]: actor writes 0,2,3, critic writes 1       */
+    int32_t grid;              /* workgroups (one per CU: 256 on MI355X)                   */
+    int32_t wgrad_splits;      /* split-K factor of the dW2 GEMM                           */
+    float* wgrad_partial;      /* f32 [wgrad_splits][256][288]                             */
+    float* grads;              /* f32 master-layout gradients: W1/W2/W3 (+ log_std) blocks */
+} dxrl_pg_fused_args;
+
+int dxrl_pg_fused_sizes(int32_t* tile_rows, int64_t* partial_floats_per_block);
+int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* args, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

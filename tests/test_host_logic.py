@@ -163,5 +163,6 @@ def test_scheduler_update_batch_equals_sequential_updates():
             assert any([a.update(bool(x), int(y)) for x, y in zip(s, st)]) == b.update_batch(s, st)
             assert a.episode_successes == b.episode_successes and a.episode_steps == b.episode_steps
             assert (a.total_steps, a.total_episodes) == (b.total_steps, b.total_episodes)
+            assert type(b.total_episodes) is int and type(b.total_steps) is int
             assert a.current_difficulty_level == b.current_difficulty_level
             assert a.progression_history == b.progression_history and a.current_config == b.current_config

@@ -23,6 +23,9 @@ for s in $STEPS; do
     pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
+    configs) for c in default hard_heldout variable_noise; do
+               run bench_$c 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-roofline
+             done ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
   esac
 done

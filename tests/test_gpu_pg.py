@@ -219,7 +219,7 @@ def test_episode_records_match_tape(pkg):
 def test_curriculum_scheduler_hook(pkg):
     """A progression decided on this iteration's records lands in the device curricula table."""
     n, T = 64, 40
-    env, tr = make(pkg, n, T, max_steps=9, record_cap=8, success_rule="training")
+    env, tr = make(pkg, n, T, max_steps=9, record_cap=T, success_rule="training")
     C = pkg.CurriculumConfig
     sched = pkg.experiments.CurriculumScheduler(C.easy(), C.hard(), success_rate_threshold=0.0,
                                                 min_episodes_before_progression=1, window_size=1,
@@ -267,10 +267,13 @@ def test_fused_dynamics_noise(pkg, std):
     jv1 = env.joint_velocities.double()
     applied = ((jv1 - np.float32(0.9) * jv0) / np.float32(0.1)).T.cpu().numpy()  # [n, 15]
     policy = np.clip(tr.act[:n, :15].cpu().numpy(), -1, 1)
+    live = tr.done[:n].cpu().numpy() == 0  # an env that finished at this step was auto-reset
+    assert live.sum() > n // 2
+    applied, policy = applied[live], policy[live]
     res = applied - policy
     if std == 0.0:
         assert np.abs(res).max() < 1e-4
     else:
         inner = res[(np.abs(applied) < 0.999) & (np.abs(policy) < 0.8)]
-        assert inner.size > 1000
+        assert inner.size > 500
         assert abs(inner.mean()) < 4e-3 and 0.046 < inner.std() < 0.054

@@ -93,6 +93,7 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(GemmArgs g) {
         const int n = n0 + wn + 32 * j + r;
         if (n >= g.N) continue;
         const float bias = g.bias ? g.bias[(int64_t)n * g.bias_stride] : 0.0f;
+        const float bk = tanh_bias(bias);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -104,12 +105,8 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(GemmArgs g) {
                     g.partial[((int64_t)blockIdx.z * g.M + m) * g.N + n] = v;
                     continue;
                 }
-                v += bias;
-                if (g.act == 1) v = tanh_f(v);
-                if (g.gate) {
-                    const float y = from_bf16(g.gate[m * g.ldg + n]);
-                    v = v * (1.0f - y * y);
-                }
+                v = g.act == 1 ? tanh_pre(v, bk) : v + bias;
+                if (g.gate) v = tanh_gate(v, from_bf16(g.gate[m * g.ldg + n]));
                 if (g.Cf) g.Cf[m * g.ldcf + n] = v;
                 if (g.Cffm) g.Cffm[(int64_t)n * g.ldffm + m] = v;
                 const bf16 vb = to_bf16(v);
@@ -203,18 +200,15 @@ __global__ __launch_bounds__(256) void k_gemm_panel(GemmArgs g) {
             const int n = wn + 32 * j + r;
             const bool nv = n < Nn;
             const float bias = (g.bias && nv) ? g.bias[(int64_t)n * g.bias_stride] : 0.0f;
+            const float bk = tanh_bias(bias);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {
                     const int row = 32 * i + acc_row(q, lane);
                     const int64_t m = m0 + row;
-                    float v = acc[i][j][q] + bias;
-                    if (g.act == 1) v = tanh_f(v);
-                    if (g.gate) {
-                        const float y = from_bf16(Gp[row * kPPitch + n]);
-                        v = v * (1.0f - y * y);
-                    }
+                    float v = g.act == 1 ? tanh_pre(acc[i][j][q], bk) : acc[i][j][q] + bias;
+                    if (g.gate) v = tanh_gate(v, from_bf16(Gp[row * kPPitch + n]));
                     if (nv && m < g.M) {
                         if (g.Cf) g.Cf[m * g.ldcf + n] = v;
                         if (g.Cffm) g.Cffm[(int64_t)n * g.ldffm + m] = v;

@@ -64,12 +64,30 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int col0, int kk, in
     return v;
 }
 
-__device__ __forceinline__ float tanh_f(float x) {
-    // tanh via exp: 1 - 2 / (exp(2x) + 1); saturates cleanly for |x| large.  The
-    // hardware reciprocal (1 ulp) replaces the IEEE division the library's
-    // correctly-rounded-division flag would otherwise emit (network math, not parity math).
-    const float e = __expf(2.0f * x);
-    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+constexpr float k2Log2e = 2.8853900817779268f;  // 2 / ln 2
+
+// Network tanh of the pre-activation acc + b:  1 - 2 / (2^((acc + b) * 2 log2 e) + 1), with the
+// bias pre-scaled (bk = tanh_bias(b)) so the exponent is one FMA and the division the hardware
+// reciprocal (network math, not parity math: 2 transcendental + 3 VALU ops).  Every kernel that
+// evaluates the MLP -- rollout, GEMM chain, fused learner -- uses exactly this sequence, so their
+// hidden units agree bit for bit (the first update's PPO ratios are exactly 1).
+__device__ __forceinline__ float tanh_bias(float b) { return b * k2Log2e; }
+__device__ __forceinline__ float tanh_pre(float acc, float bk) {
+    const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(acc, k2Log2e, bk));
+    return __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
 }
+// Two lanes' worth of the same sequence on packed f32 ops (v_pk_fma_f32 / v_pk_add_f32: bit
+// for bit the scalar results, half the VALU issue slots)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 tanh_pre2(f32x2 acc, f32x2 bk) {
+    const f32x2 x = __builtin_elementwise_fma(acc, f32x2{k2Log2e, k2Log2e}, bk);
+    const f32x2 d = f32x2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)} + 1.0f;
+    const f32x2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    return __builtin_elementwise_fma(r, f32x2{-2.0f, -2.0f}, f32x2{1.0f, 1.0f});
+}
+__device__ __forceinline__ f32x2 tanh_gate2(f32x2 g, f32x2 y) { return __builtin_elementwise_fma(-(g * y), y, g); }
+
+// tanh' gate of a back-propagated gradient: g (1 - y^2) as one multiply + one FMA
+__device__ __forceinline__ float tanh_gate(float g, float y) { return __builtin_fmaf(-(g * y), y, g); }
 
 }  // namespace dxrl

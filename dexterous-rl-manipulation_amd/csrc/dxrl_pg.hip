@@ -176,12 +176,12 @@ __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfr
     for (int j = 0; j < NT; ++j) {
         const int n = n0 + 32 * j + r;
         const float bias = bias_p ? bias_p[(int64_t)n * ldb] : 0.0f;
+        const float bk = tanh_bias(bias);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                float v = acc[i][j][q] + bias;
-                if (kTanh) v = tanh_f(v);
+                const float v = kTanh ? tanh_pre(acc[i][j][q], bk) : acc[i][j][q] + bias;
                 out[(32 * i + acc_row(q, lane)) * ldo + n] = to_bf16(v);
             }
     }

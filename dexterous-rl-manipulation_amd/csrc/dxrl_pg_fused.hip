@@ -28,6 +28,11 @@
 #include "dxrl_gemm.h"
 #include "dxrl_pg.h"
 
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+
 using namespace dxrl;
 using namespace dxrl::pg;
 
@@ -36,9 +41,6 @@ namespace {
 
 constexpr float kLog2PiF = 1.8378770664093453f;
 constexpr int kTR = 128;                 // samples per tile
-constexpr int kFW = 4;                   // waves per workgroup: one per SIMD, 512 registers each
-constexpr int kFThreads = 64 * kFW;
-constexpr int kNT = kH / 32 / kFW;       // 32-wide feature tiles per wave (2)
 constexpr int kXp = kIn + 8;             // 72:  X rows (conflict-free b128 row reads)
 constexpr int kHp = kH + 8;              // 264: H1 / H2 rows
 constexpr int kDp = kOut + 8;            // 40:  dout rows
@@ -48,7 +50,7 @@ constexpr int kOffH2 = kOffH1 + kTR * kHp;
 constexpr int kOffD = kOffH2 + kTR * kHp;
 constexpr int kLdsElems = kOffD + kTR * kDp;
 static_assert(kLdsElems * 2 == 163840, "the fused kernel uses exactly the CU's 160 KiB of LDS");
-static_assert(kTR / 32 == kFW, "one 32-sample head tile per wave");
+constexpr int kHW = kTR / 32;            // waves running the heads (one 32-sample tile each)
 
 // per-workgroup gradient partial slab (f32)
 constexpr int kPartW1 = 0;                   // [256][64]
@@ -56,9 +58,16 @@ constexpr int kPartW3 = kPartW1 + kH * kIn;  // [32][288]
 constexpr int kPartLs = kPartW3 + kOut * kHx;
 constexpr int kPartSize = kPartLs + 16;
 
+// global-address-space views: loads through them compile to global_load (vmcnt only); a
+// generic pointer the compiler cannot place compiles to flat_load, which also counts in
+// lgkmcnt and so holds every LDS wait until the global data is back
+typedef __attribute__((address_space(1))) const bf16x8 gbf16x8;
+typedef __attribute__((address_space(1))) const float gf32;
+
 struct FusedArgs {
     int net;    // 0 actor, 1 critic
     int train;  // 0: forward only (critic values), 1: forward + heads + backward
+    int diag;   // timing ablations (DXRL_FUSED_DIAG): 1 no HBM copies, 4 no dW MFMAs, 8 stamps
     int64_t rows;
     const bf16* X;  // [rows][64], column 45 = 1
     const bf16 *W1, *W2, *W3, *W2T, *W3T;
@@ -76,6 +85,7 @@ struct FusedArgs {
     bf16* dh2_out;  // [rows][kH]
     float* part;    // [grid][kPartSize]
     double* loss;   // [grid][4]
+    unsigned long long* stamps;  // diag & 8: [grid][waves][16] cycles per segment
 };
 
 __device__ __forceinline__ void zero_acc(f32x16& a) {
@@ -89,41 +99,37 @@ __device__ __forceinline__ void zero_acc(f32x16& a) {
 template <int KS, int kLda, int NT>
 __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int ldw, int ft0, const bf16* A,
                                           f32x16 (&acc)[NT][4], int lane) {
+    static_assert(NT == 1, "one feature tile per call");
     const int r = lane & 31, h = lane >> 5;
-    constexpr int kC = KS < 4 ? KS : 4;  // k-steps per chunk
-    static_assert(KS % kC == 0, "chunking");
+    constexpr int kD = KS < 8 ? KS : 8;  // weight prefetch distance (k-steps)
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
+    for (int mt = 0; mt < 4; ++mt) zero_acc(acc[0][mt]);
+    // weights through the global address space (global_load: vmcnt only -- a flat load would
+    // also hold every LDS wait), kD k-steps ahead
+    const gbf16x8* wp = (const gbf16x8*)(W + (int64_t)(32 * ft0 + r) * ldw + 8 * h);
+    bf16x8 wf[kD];
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) zero_acc(acc[j][mt]);
-    const bf16* wp[NT];
+    for (int k = 0; k < kD; ++k) wf[k] = wp[2 * k];
+    // activation fragments double-buffered one k-step ahead
+    const bf16* ap = A + r * kLda + 8 * h;
+    bf16x8 bq[2][4];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) wp[j] = W + (int64_t)(32 * (ft0 + j) + r) * ldw + 8 * h;
-    bf16x8 cur[kC][NT], nxt[kC][NT];
+    for (int mt = 0; mt < 4; ++mt) bq[0][mt] = *reinterpret_cast<const bf16x8*>(ap + 32 * mt * kLda);
 #pragma unroll
-    for (int k = 0; k < kC; ++k)
+    for (int k = 0; k < KS; ++k) {
+        if (k + 1 < KS) {
 #pragma unroll
-        for (int j = 0; j < NT; ++j) cur[k][j] = *reinterpret_cast<const bf16x8*>(wp[j] + 16 * k);
-#pragma unroll 1
-    for (int kc = 0; kc < KS; kc += kC) {
-        if (kc + kC < KS) {
-#pragma unroll
-            for (int k = 0; k < kC; ++k)
-#pragma unroll
-                for (int j = 0; j < NT; ++j) nxt[k][j] = *reinterpret_cast<const bf16x8*>(wp[j] + 16 * (kc + kC + k));
+            for (int mt = 0; mt < 4; ++mt)
+                bq[(k + 1) & 1][mt] = *reinterpret_cast<const bf16x8*>(ap + 32 * mt * kLda + 16 * (k + 1));
         }
+        const bf16x8 a = wf[k % kD];
+        if (k + kD < KS) wf[k % kD] = wp[2 * (k + kD)];
+        // keep the prefetches above issued ahead of this k-step's MFMAs (the scheduler would
+        // otherwise sink every load next to its use and expose its full latency)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int k = 0; k < kC; ++k)
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-                const bf16x8 b = *reinterpret_cast<const bf16x8*>(A + (32 * mt + r) * kLda + 16 * (kc + k) + 8 * h);
-#pragma unroll
-                for (int j = 0; j < NT; ++j) acc[j][mt] = mfma32(cur[k][j], b, acc[j][mt]);
-            }
-#pragma unroll
-        for (int k = 0; k < kC; ++k)
-#pragma unroll
-            for (int j = 0; j < NT; ++j) cur[k][j] = nxt[k][j];
+        for (int mt = 0; mt < 4; ++mt) acc[0][mt] = mfma32(a, bq[k & 1][mt], acc[0][mt]);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -138,13 +144,18 @@ __device__ __forceinline__ void store_hidden(const f32x16 (&acc)[1][4], int ft, 
             float b[4] = {0.0f, 0.0f, 0.0f, 0.0f};
             if (bias) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) b[u] = bias[(int64_t)(f0 + u) * kHx];
+                for (int u = 0; u < 4; ++u) b[u] = tanh_bias(((gf32*)bias)[(int64_t)(f0 + u) * kHx]);
             }
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
                 bf16x4 v;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = to_bf16(tanh_f(acc[j][mt][4 * g + u] + b[u]));
+                for (int u = 0; u < 4; u += 2) {
+                    const f32x2 t = tanh_pre2(f32x2{acc[j][mt][4 * g + u], acc[j][mt][4 * g + u + 1]},
+                                              f32x2{b[u], b[u + 1]});
+                    v[u] = to_bf16(t.x);
+                    v[u + 1] = to_bf16(t.y);
+                }
                 *reinterpret_cast<bf16x4*>(H + (32 * mt + r) * kHp + f0) = v;
             }
         }
@@ -163,16 +174,32 @@ __device__ __forceinline__ void gate_in_place(const f32x16 (&acc)[1][4], int ft,
                 const bf16x4 y = *yp;
                 bf16x4 v;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const float yy = from_bf16(y[u]);
-                    v[u] = to_bf16(acc[j][mt][4 * g + u] * (1.0f - yy * yy));
+                for (int u = 0; u < 4; u += 2) {
+                    const f32x2 t = tanh_gate2(f32x2{acc[j][mt][4 * g + u], acc[j][mt][4 * g + u + 1]},
+                                               f32x2{from_bf16(y[u]), from_bf16(y[u + 1])});
+                    v[u] = to_bf16(t.x);
+                    v[u + 1] = to_bf16(t.y);
                 }
                 *yp = v;
             }
         }
 }
 
-__global__ __launch_bounds__(kFThreads, 1) void k_pg_fused(FusedArgs p) {
+// Hide a pointer's provenance from the optimiser so loads through it are not hoisted
+// out of the tile loop (loop-invariant weight / bias loads would otherwise pin registers
+// for the whole launch).
+template <typename T>
+__device__ __forceinline__ T* opaque(T* ptr) {
+    asm volatile("" : "+s"(ptr));
+    return ptr;
+}
+
+// kFW waves per workgroup: 4 (one per SIMD, 512 registers each) or 8 (two per SIMD)
+template <int kFW>
+__global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
+    constexpr int kFThreads = 64 * kFW;
+    constexpr int kNT = kH / 32 / kFW;  // 32-wide feature tiles per wave
+    static_assert(kHW <= kFW, "one 32-sample head tile per wave");
     __shared__ __attribute__((aligned(16))) bf16 lds[kLdsElems];
     bf16* X = lds + kOffX;
     bf16* H1 = lds + kOffH1;
@@ -210,42 +237,67 @@ __global__ __launch_bounds__(kFThreads, 1) void k_pg_fused(FusedArgs p) {
             xr[u] = m < p.rows ? *reinterpret_cast<const bf16x8*>(p.X + m * kIn + col) : zero8();
         }
     };
+    unsigned long long st_acc[16], st_last = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) st_acc[k] = 0;
+#define STAMP(k)                                                                                 \
+    do {                                                                                         \
+        if (p.diag & 8) {                                                                        \
+            __builtin_amdgcn_sched_barrier(0);                                                   \
+            unsigned long long t_;                                                               \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+            __builtin_amdgcn_sched_barrier(0);                                                   \
+            st_acc[k] += t_ - st_last;                                                           \
+            st_last = t_;                                                                        \
+        }                                                                                        \
+    } while (0)
     int64_t tile = blockIdx.x;
     if (tile < ntiles) fetch_x(tile);
+    STAMP(15);
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t m0 = tile * kTR;
+        const bf16 *W1 = opaque(p.W1), *W2 = opaque(p.W2), *W3 = opaque(p.W3), *W2T = opaque(p.W2T),
+                   *W3T = opaque(p.W3T);
+        const float *b2 = opaque(p.b2), *b3 = opaque(p.b3), *logstd = opaque(p.logstd);
 #pragma unroll
         for (int u = 0; u < kXU; ++u) {
             const int c = tid + kFThreads * u, row = c >> 3, col = 8 * (c & 7);
             *reinterpret_cast<bf16x8*>(X + row * kXp + col) = xr[u];
         }
+        STAMP(0);
         __syncthreads();
-        if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
+        STAMP(1);
+        // (the next tile's X is fetched late in this one: vmcnt retires in issue order, so an
+        // HBM load issued here would make every weight-fragment wait below wait for it too)
 
         // ---- L1, L2 (wave w: hidden features 64w .. 64w + 63, all 128 samples)
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[1][4];
-            fwd_tiles<kIn / 16, kXp, 1>(p.W1, kIn, ft0 + j, X, acc, lane);  // bias = W1 column 45 (X column 45 = 1)
+            fwd_tiles<kIn / 16, kXp, 1>(W1, kIn, ft0 + j, X, acc, lane);  // bias = W1 column 45 (X column 45 = 1)
             store_hidden(acc, ft0 + j, nullptr, H1, lane);
         }
+        STAMP(2);
         __syncthreads();
+        STAMP(3);
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[1][4];
-            fwd_tiles<kH / 16, kHp, 1>(p.W2, kHx, ft0 + j, H1, acc, lane);
-            store_hidden(acc, ft0 + j, p.b2, H2, lane);
+            fwd_tiles<kH / 16, kHp, 1>(W2, kHx, ft0 + j, H1, acc, lane);
+            store_hidden(acc, ft0 + j, b2, H2, lane);
         }
+        STAMP(4);
         __syncthreads();
+        STAMP(5);
 
-        // ---- head: wave w owns samples 32w .. 32w + 31 (lane: sample r, head rows of half h)
-        {
+        // ---- head: wave w < kHW owns samples 32w .. 32w + 31 (lane: sample r, head rows of half h)
+        if (wave < kHW) {
             f32x16 acc;
             zero_acc(acc);
-            const bf16* wrow = p.W3 + (int64_t)r * kHx + 8 * h;
+            const gbf16x8* wrow = (const gbf16x8*)(W3 + (int64_t)r * kHx + 8 * h);
 #pragma unroll
             for (int k = 0; k < kH / 16; ++k) {
-                const bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + 16 * k);
+                const bf16x8 a = wrow[2 * k];
                 const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * k + 8 * h);
                 acc = mfma32(a, b, acc);
             }
@@ -256,7 +308,7 @@ __global__ __launch_bounds__(kFThreads, 1) void k_pg_fused(FusedArgs p) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 d[q] = 0.0f;
-                b3v[q] = p.b3[(int64_t)((q & 3) + 8 * (q >> 2) + 4 * h) * kHx];  // head row o of register q
+                b3v[q] = ((gf32*)b3)[(int64_t)((q & 3) + 8 * (q >> 2) + 4 * h) * kHx];  // head row o of register q
             }
             if (p.net == 0) {
                 if (p.train) {
@@ -264,7 +316,7 @@ __global__ __launch_bounds__(kFThreads, 1) void k_pg_fused(FusedArgs p) {
 #pragma unroll
                     for (int q = 0; q < 8; ++q) {
                         const int o = (q & 3) + 8 * (q >> 2) + 4 * h;
-                        lsv[q] = o < kAct ? p.logstd[o] : 0.0f;
+                        lsv[q] = o < kAct ? ((gf32*)logstd)[o] : 0.0f;
                         iv2[q] = __expf(-2.0f * lsv[q]);
                     }
                     float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
@@ -345,8 +397,11 @@ __global__ __launch_bounds__(kFThreads, 1) void k_pg_fused(FusedArgs p) {
                 }
             }
         }
+        STAMP(6);
         if (!p.train) {
+            if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
             __syncthreads();  // X / H1 / H2 are rewritten by the next tile
+            STAMP(7);
             continue;
         }
         // H1 tile -> HBM (B operand of the dW2 GEMM): 128 rows x 32 chunks of 16 B
@@ -354,43 +409,51 @@ __global__ __launch_bounds__(kFThreads, 1) void k_pg_fused(FusedArgs p) {
         for (int c = tid; c < kTR * (kH / 8); c += kFThreads) {
             const int row = c >> 5, col = 8 * (c & 31);
             const int64_t m = m0 + row;
-            if (m < p.rows)
+            if (m < p.rows && !(p.diag & 1))
                 *reinterpret_cast<bf16x8*>(p.h1_out + m * kHx + col) = *reinterpret_cast<const bf16x8*>(H1 + row * kHp + col);
         }
+        STAMP(7);
         __syncthreads();
+        STAMP(8);
 
         // ---- dW3 += dout^T H2 (wave w: H2 columns of its tiles), then dH2 in place of H2
 #pragma unroll
         for (int kk = 0; kk < kTR; kk += 16) {
             const bf16x8 a = tr_frag<kDp>(D, 0, kk, lane);
 #pragma unroll
-            for (int j = 0; j < kNT; ++j) acc3[j] = mfma32(a, tr_frag<kHp>(H2, 32 * (ft0 + j), kk, lane), acc3[j]);
+            for (int j = 0; j < kNT; ++j) if (!(p.diag & 4)) acc3[j] = mfma32(a, tr_frag<kHp>(H2, 32 * (ft0 + j), kk, lane), acc3[j]);
         }
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[1][4];
-            fwd_tiles<kOut / 16, kDp, 1>(p.W3T, kOut, ft0 + j, D, acc, lane);  // dH2^T = W3^T dout^T
+            fwd_tiles<kOut / 16, kDp, 1>(W3T, kOut, ft0 + j, D, acc, lane);  // dH2^T = W3^T dout^T
             gate_in_place(acc, ft0 + j, H2, lane);
         }
+        STAMP(9);
         __syncthreads();
+        STAMP(10);
 
         // ---- dH2 -> HBM; dH1 = (dH2 W2) * (1 - H1^2)  (wave w: L2 inputs of its tiles, rows = samples)
 #pragma unroll 4
         for (int c = tid; c < kTR * (kH / 8); c += kFThreads) {
             const int row = c >> 5, col = 8 * (c & 31);
             const int64_t m = m0 + row;
-            if (m < p.rows)
+            if (m < p.rows && !(p.diag & 1))
                 *reinterpret_cast<bf16x8*>(p.dh2_out + m * kH + col) = *reinterpret_cast<const bf16x8*>(H2 + row * kHp + col);
         }
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[1][4];
-            fwd_tiles<kH / 16, kHp, 1>(p.W2T, kH, ft0 + j, H2, acc, lane);  // dH1^T = W2^T dH2^T
+            fwd_tiles<kH / 16, kHp, 1>(W2T, kH, ft0 + j, H2, acc, lane);  // dH1^T = W2^T dH2^T
             gate_in_place(acc, ft0 + j, H1, lane);                             // H1 is in HBM already
         }
+        STAMP(11);
         __syncthreads();
+        STAMP(12);
 
-        // ---- dW1 += dH1^T X (wave w: hidden rows of its tiles, input columns 0..63)
+        // ---- dW1 += dH1^T X (wave w: hidden rows of its tiles, input columns 0..63); LDS only,
+        //      so the next tile's X loads go out now
+        if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
 #pragma unroll
         for (int kk = 0; kk < kTR; kk += 16) {
             bf16x8 b[2];
@@ -400,11 +463,18 @@ __global__ __launch_bounds__(kFThreads, 1) void k_pg_fused(FusedArgs p) {
             for (int j = 0; j < kNT; ++j) {
                 const bf16x8 a = tr_frag<kHp>(H1, 32 * (ft0 + j), kk, lane);
 #pragma unroll
-                for (int it = 0; it < 2; ++it) acc1[j][it] = mfma32(a, b[it], acc1[j][it]);
+                for (int it = 0; it < 2; ++it) if (!(p.diag & 4)) acc1[j][it] = mfma32(a, b[it], acc1[j][it]);
             }
         }
+        STAMP(13);
         __syncthreads();
+        STAMP(14);
     }
+    if ((p.diag & 8) && lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) p.stamps[((int64_t)blockIdx.x * kFW + wave) * 16 + k] = st_acc[k];
+    }
+#undef STAMP
     if (!p.train) return;
 
     // ---- workgroup partials (fixed layout; reduced in block order by k_fused_reduce)
@@ -418,21 +488,23 @@ __global__ __launch_bounds__(kFThreads, 1) void k_pg_fused(FusedArgs p) {
 #pragma unroll
             for (int it = 0; it < 2; ++it) part[kPartW1 + (32 * (ft0 + j) + o) * kIn + 32 * it + r] = acc1[j][it][q];
         }
-    float* red = reinterpret_cast<float*>(lds);              // [256 lanes][16]
-    double* lred = reinterpret_cast<double*>(lds + kOffH1);  // [256 lanes][4]
+    float* red = reinterpret_cast<float*>(lds);              // [head lanes][16]
+    double* lred = reinterpret_cast<double*>(lds + kOffH1);  // [head lanes][4]
+    if (wave < kHW) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        red[tid * 16 + q] = dls[q];
-        red[tid * 16 + 8 + q] = db3[q];
+        for (int q = 0; q < 8; ++q) {
+            red[tid * 16 + q] = dls[q];
+            red[tid * 16 + 8 + q] = db3[q];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lred[tid * 4 + k] = lsum[k];
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) lred[tid * 4 + k] = lsum[k];
     __syncthreads();
     if (tid < 32) {  // head row o: lanes with h = (o >> 2) & 1, register q = (o & 3) + 4 (o >> 3)
         const int o = tid, hh = (o >> 2) & 1, q = (o & 3) + 4 * (o >> 3);
         float sl = 0.0f, sb = 0.0f;
         if (o < 16) {
-            for (int w = 0; w < kFW; ++w)
+            for (int w = 0; w < kHW; ++w)
                 for (int rr = 0; rr < 32; ++rr) {
                     const int t = 64 * w + 32 * hh + rr;
                     sl += red[t * 16 + q];
@@ -444,7 +516,7 @@ __global__ __launch_bounds__(kFThreads, 1) void k_pg_fused(FusedArgs p) {
     } else if (tid < 36) {
         const int k = tid - 32;
         double s = 0.0;
-        for (int t = 0; t < kFThreads; ++t) s += lred[t * 4 + k];
+        for (int t = 0; t < 64 * kHW; ++t) s += lred[t * 4 + k];
         if ((p.net == 0) == (k != 1)) p.loss[(int64_t)blockIdx.x * 4 + k] = s;
     }
 }
@@ -528,8 +600,33 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     f.loss = a->loss_partial;
     const int64_t ntiles = (a->rows + kTR - 1) / kTR;
     const int grid = (int)(ntiles < a->grid ? ntiles : a->grid);
-    hipLaunchKernelGGL(k_pg_fused, dim3(grid), dim3(kFThreads), 0, st, f);
+    static const int diag = [] {
+        const char* v = getenv("DXRL_FUSED_DIAG");
+        return v ? atoi(v) : 0;
+    }();
+    f.diag = diag;
+    static const int waves = [] {
+        const char* v = getenv("DXRL_FUSED_WAVES");
+        return v && atoi(v) == 8 ? 8 : 4;
+    }();
+    static unsigned long long* stamps = nullptr;
+    if ((diag & 8) && !stamps) (void)hipMalloc(&stamps, (size_t)65536 * 8 * 16 * 8);
+    f.stamps = stamps;
+    if (waves == 8) hipLaunchKernelGGL(k_pg_fused<8>, dim3(grid), dim3(512), 0, st, f);
+    else hipLaunchKernelGGL(k_pg_fused<4>, dim3(grid), dim3(256), 0, st, f);
     if (int rc = launch_check("k_pg_fused")) return rc;
+    if (diag & 8) {  // print the mean cycles per segment per wave (diagnostic builds only)
+        std::vector<unsigned long long> h((size_t)grid * waves * 16);
+        (void)hipStreamSynchronize(st);
+        (void)hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost);
+        fprintf(stderr, "fused net=%d train=%d waves=%d cycles/wave:", a->net, (int)train, waves);
+        for (int k = 0; k < 16; ++k) {
+            double sum = 0;
+            for (size_t w = 0; w < (size_t)grid * waves; ++w) sum += (double)h[w * 16 + k];
+            fprintf(stderr, " s%d=%.0f", k, sum / (grid * waves));
+        }
+        fprintf(stderr, "\n");
+    }
     if (!train) return DXRL_OK;
     float* G = a->grads;
     hipLaunchKernelGGL(k_fused_reduce, dim3((kPartSize + 255) / 256), dim3(256), 0, st, a->partial, grid,

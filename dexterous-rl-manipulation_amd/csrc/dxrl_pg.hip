@@ -149,27 +149,29 @@ __device__ __forceinline__ void load_wtile(WTile<KS>& w, const bf16* W, int ldw,
 // One wave: 64 rows x 32*NT columns of act(A . W^T + b) into LDS.  A: LDS [64][lda]
 // bf16; the weight fragment of N-tile j, k-step k comes from wfrag(j, k) (registers
 // or LDS); bias: f32 master column (bias[n * ldb]), the values the training GEMMs use.
-template <int KS, int NT, bool kTanh, typename WF>
+template <int KS, int NT, bool kTanh, int RT = 2, typename WF>
 __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfrag, int n0, const float* bias_p,
                                            int ldb, bf16* out, int ldo, int lane) {
+    // RT row tiles of 32 (RT == 1: 16 live rows -- accumulator registers q < 8)
+    constexpr int kQ = RT == 1 ? 8 : 16;
     const int r = lane & 31, h = lane >> 5;
-    f32x16 acc[2][NT];
+    f32x16 acc[RT][NT];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.0f;
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
-        bf16x8 a[2];
+        bf16x8 a[RT];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const bf16x8*>(A + (32 * i + r) * lda + 16 * k + 8 * h);
+        for (int i = 0; i < RT; ++i) a[i] = *reinterpret_cast<const bf16x8*>(A + (32 * i + r) * lda + 16 * k + 8 * h);
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
             const bf16x8 b = wfrag(j, k);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) acc[i][j] = mfma32(a[i], b, acc[i][j]);
+            for (int i = 0; i < RT; ++i) acc[i][j] = mfma32(a[i], b, acc[i][j]);
         }
     }
 #pragma unroll
@@ -178,9 +180,9 @@ __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfr
         const float bias = bias_p ? bias_p[(int64_t)n * ldb] : 0.0f;
         const float bk = tanh_bias(bias);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < RT; ++i)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
+            for (int q = 0; q < kQ; ++q) {
                 const float v = kTanh ? tanh_pre(acc[i][j][q], bk) : acc[i][j][q] + bias;
                 out[(32 * i + acc_row(q, lane)) * ldo + n] = to_bf16(v);
             }
@@ -349,6 +351,355 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout(PgRolloutA
         p.ep_sum_ret[i] = sum_ret;
         p.ep_sum_len[i] = sum_len;
         p.ep_succ[i] = succ;
+    }
+}
+
+// ------------------------------------------------------------------ lane-split rollout
+// k_pg_rollout_ls: the same rollout as k_pg_rollout (same Philox streams and counters, the
+// same arithmetic, so the two kernels write bit-identical tapes), re-laid-out for latency.
+// A workgroup owns 16 envs (4096 envs -> 256 workgroups, one per CU) and each env is spread
+// over 16 lanes of one wave: lane s owns joint s (jp, jv), lanes 0..2 the object's axis s,
+// and every lane keeps a copy of the env's scalars (flags, step, size, mass, friction ...).
+// Elementwise physics runs lane-parallel; the reference's ordered sums (finger sums, the
+// closure term, log pi) are gathered with in-group shuffles and added in the reference order
+// on every lane.  The actor MLP runs on all four waves as in k_pg_rollout, on one 32-row
+// MFMA tile of which rows 0..15 are this workgroup's envs.
+constexpr int kLsEnvs = 16, kLsLanes = 16;
+
+template <typename T>
+__device__ __forceinline__ T gshfl(T v, int src) {  // value of lane `src` of this 16-lane group
+    return __shfl(v, src, kLsLanes);
+}
+__device__ __forceinline__ double gshfl(double v, int src) {
+    const int2 b = *reinterpret_cast<int2*>(&v);
+    const int2 r{__shfl(b.x, src, kLsLanes), __shfl(b.y, src, kLsLanes)};
+    return *reinterpret_cast<const double*>(&r);
+}
+
+// standard normal k of Philox block k / 4 (Box-Muller pairs (x, y), (z, w)), as philox_normals
+__device__ __forceinline__ float philox_normal_at(int k, uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream) {
+    const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)(k >> 2)}, k0, k1);
+    float n0, n1;
+    if ((k & 2) == 0) box_muller(r.x, r.y, n0, n1);
+    else box_muller(r.z, r.w, n0, n1);
+    return (k & 1) ? n1 : n0;
+}
+
+// 53-bit uniform of reset slot k (Philox block k / 2, half k % 2), as env_reset_philox
+__device__ __forceinline__ double reset_uniform_at(int k, uint32_t k0, uint32_t k1, uint64_t ctr) {
+    const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamReset, (uint32_t)(k >> 1)}, k0, k1);
+    return (k & 1) ? u01_53(r.z, r.w) : u01_53(r.x, r.y);
+}
+
+// Lane-split contacts_of: every lane of the group gets the mask and the minimum distance.
+// gbit: this group's bit offset in the wave's ballot.
+__device__ __forceinline__ uint32_t ls_contacts(float jp, const double op[3], double size, int s, int gbit,
+                                                double& dmin, float g3[3]) {
+    const int f = s < kF ? s : 0;
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) g3[j] = gshfl(jp, kJ * f + j);
+    float sum = g3[0];
+#pragma unroll
+    for (int j = 1; j < kJ; ++j) sum = sum + g3[j];
+    const double tip = (double)(sum * kC01);
+    const double dx = tip - op[0], dy = tip - op[1], dz = tip - op[2];
+    const double d = sqrt((dx * dx + dy * dy) + dz * dz);
+    const bool hit = s < kF && d < size * 1.5;
+    const uint32_t mask = (uint32_t)(__ballot(hit) >> gbit) & ((1u << kF) - 1u);
+    dmin = gshfl(d, 0);
+#pragma unroll
+    for (int k = 1; k < kF; ++k) {
+        const double dk = gshfl(d, k);
+        dmin = dk < dmin ? dk : dmin;
+    }
+    return mask;
+}
+
+__global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRolloutArgs p) {
+    constexpr int kRows = 32;  // MFMA row tile; rows >= kLsEnvs are padding
+    __shared__ __attribute__((aligned(16))) bf16 W1s[kH * kW1s];
+    __shared__ __attribute__((aligned(16))) bf16 W3s[kOut * kW3s];
+    __shared__ __attribute__((aligned(16))) bf16 X[kRows * kXs];
+    __shared__ __attribute__((aligned(16))) bf16 H1[kRows * kHs];
+    __shared__ __attribute__((aligned(16))) bf16 H2[kRows * kHs];
+    __shared__ float MU[kLsEnvs * (kOut + 1)];
+    __shared__ float LS[kActPad], SIG[kActPad], ISIG[kActPad];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int eg = tid >> 4, s = tid & 15, gbit = 16 * (eg & 3);
+    const int64_t n = p.s.n;
+    const int64_t i = (int64_t)blockIdx.x * kLsEnvs + eg;
+    const bool live = i < n;
+    const int64_t T = p.horizon;
+    if (tid < kAct) {
+        const float ls = p.params[kOffLogStd + tid];
+        LS[tid] = ls;
+        SIG[tid] = __expf(ls);
+        ISIG[tid] = __expf(-ls);
+    }
+    WTile<kH / 16> w2[kNT];
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) load_wtile(w2[j], p.wbf + kBfW2a, kHx, kCpw * wave + 32 * j, lane);
+    for (int c = tid; c < kH * (kIn / 8); c += 64 * kRolloutWaves) {
+        const int row = c / (kIn / 8), col = 8 * (c % (kIn / 8));
+        *reinterpret_cast<bf16x8*>(W1s + row * kW1s + col) =
+            *reinterpret_cast<const bf16x8*>(p.wbf + kBfW1a + (int64_t)row * kIn + col);
+    }
+    for (int c = tid; c < kOut * (kH / 8); c += 64 * kRolloutWaves) {
+        const int row = c / (kH / 8), col = 8 * (c % (kH / 8));
+        *reinterpret_cast<bf16x8*>(W3s + row * kW3s + col) =
+            *reinterpret_cast<const bf16x8*>(p.wbf + kBfW3a + (int64_t)row * kHx + col);
+    }
+    // padding rows and the constant columns of the X tile (bias column 45 = 1)
+    for (int c = tid; c < kRows * kXs; c += 64 * kRolloutWaves) {
+        const int row = c / kXs, col = c % kXs;
+        X[c] = (row < kLsEnvs && col == kObsIn) ? (bf16)1.0f : (bf16)0.0f;
+    }
+    for (int c = tid; c < (kRows - kLsEnvs) * kHs; c += 64 * kRolloutWaves) {
+        H1[kLsEnvs * kHs + c] = (bf16)0.0f;
+        H2[kLsEnvs * kHs + c] = (bf16)0.0f;
+    }
+    const int r32 = lane & 31, h2 = lane >> 5;
+    const auto w1frag = [&](int j, int k) {
+        return *reinterpret_cast<const bf16x8*>(W1s + (kCpw * wave + 32 * j + r32) * kW1s + 16 * k + 8 * h2);
+    };
+    const auto w2frag = [&](int j, int k) { return w2[j].b[k]; };
+
+    // ---- per-lane env state
+    float jp = 0.0f, jv = 0.0f;  // joint s
+    double opd = 0.0;            // object axis s (s < 3)
+    float ovd = 0.0f;
+    uint32_t flags = 0;
+    int32_t et = 0, cfg = 0;
+    double size = 0.0, mass = 0.0, fric = 0.0, ep_ret = 0.0, sum_ret = 0.0;
+    int32_t cnt = 0, sum_len = 0, succ = 0;
+    uint64_t rctr = 0;
+    uint32_t ek0 = 0, ek1 = 0, pk0 = 0, pk1 = 0;
+    if (live) {
+        if (s < kD) {
+            jp = p.s.jp[(int64_t)s * n + i];
+            jv = p.s.jv[(int64_t)s * n + i];
+        }
+        if (s < 3) {
+            opd = p.s.op[(int64_t)s * n + i];
+            ovd = p.s.ov[(int64_t)s * n + i];
+        }
+        flags = p.s.flags[i];
+        et = p.s.t[i];
+        size = p.s.size[i];
+        mass = p.s.mass[i];
+        fric = p.s.fric[i];
+        cfg = p.s.cfg[i];
+        ep_ret = p.ep_ret[i];
+        rctr = p.s.reset_ctr[i];
+        env_key(p.env_seed, p.gid0 + i, ek0, ek1);
+        env_key(p.policy_seed, p.gid0 + i, pk0, pk1);
+    }
+    // observation row of this env (+ observation noise): lane s writes jp[s], jv[s], the
+    // object axis s, a quaternion slot and a contact bit -- element k of ME:254-264
+    const auto write_obs_row = [&](uint64_t ctr) {
+        bf16* xr = X + eg * kXs;
+        const auto put = [&](int k, float v) {
+            if (p.obs_noise > 0.0f) v = v + p.obs_noise * philox_normal_at(k, pk0, pk1, ctr, kStreamObs);
+            xr[k] = to_bf16(v);
+        };
+        if (s < kD) {
+            put(s, jp);
+            put(kD + s, jv);
+        }
+        if (s < 3) {
+            put(2 * kD + s, (float)opd);
+            put(2 * kD + 7 + s, ovd);
+        } else if (s < 7) {
+            put(2 * kD + s, s == 3 ? 1.0f : 0.0f);  // identity quaternion (ME:164)
+        } else if (s < 7 + kF) {
+            put(2 * kD + 10 + (s - 7), (float)((flags >> (s - 7)) & 1u));
+        }
+    };
+    const auto tape_obs_row = [&](int64_t m) {  // 64 bf16 = 16 lanes x 8 bytes
+        *reinterpret_cast<bf16x4*>(p.obs_rm + m * kIn + 4 * s) = *reinterpret_cast<const bf16x4*>(X + eg * kXs + 4 * s);
+    };
+    const bool mlp = !(p.diag & 1);
+    for (int64_t t = 0; t < T; ++t) {
+        const int64_t m = t * n + i;
+        const uint64_t ctr = p.iteration * (uint64_t)T + (uint64_t)t;
+        if (live) write_obs_row(ctr);
+        __syncthreads();
+        if (live) tape_obs_row(m);
+        if (mlp) wave_layer<kIn / 16, kNT, true, 1>(X, kXs, w1frag, kCpw * wave, nullptr, 0, H1, kHs, lane);
+        __syncthreads();
+        if (mlp) wave_layer<kH / 16, kNT, true, 1>(H1, kHs, w2frag, kCpw * wave, p.params + kOffW2a + kH, kHx, H2,
+                                                  kHs, lane);
+        __syncthreads();
+        if (mlp && wave == kRolloutWaves - 1) {  // mu head: 16 env rows x 32 head rows
+            f32x16 acc;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kH / 16; ++k) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(H2 + r32 * kHs + 16 * k + 8 * h2);
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(W3s + r32 * kW3s + 16 * k + 8 * h2);
+                acc = mfma32(a, b, acc);
+            }
+            const float bias = p.params[kOffW3a + (int64_t)r32 * kHx + kH];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) MU[acc_row(q, lane) * (kOut + 1) + r32] = acc[q] + bias;  // rows < 16
+        }
+        __syncthreads();
+        if (!live) continue;
+        // ---- a = mu + sigma * eps, log pi(a|s) in action order (gauss_logp's order)
+        const int sa = s < kAct ? s : 0;
+        const float mu = mlp ? MU[eg * (kOut + 1) + sa] : 0.0f;
+        float a = mu + SIG[sa] * philox_normal_at(sa, pk0, pk1, ctr, kStreamPolicy);
+        const float z = (a - mu) * ISIG[sa];
+        const float term = -0.5f * z * z - LS[sa] - 0.5f * kLog2Pi;
+        float lp = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kAct; ++k) lp += gshfl(term, k);
+        p.act[m * kActPad + s] = s < kAct ? a : 0.0f;
+        if (s == 0) p.logp[m] = lp;
+        if (p.dyn_noise > 0.0f)  // robustness_tests.py:180-187 (the tape keeps the policy's action)
+            a = clipf(a + p.dyn_noise * philox_normal_at(sa, pk0, pk1, ctr, kStreamDyn), -1.0f, 1.0f);
+        bool te = false, tr = false;
+        double r = 0.0;
+        if (!(p.diag & 2)) {
+            // ---- env_step, lane-split (ME:198-252)
+            if (s < kD) {
+                const float ak = clipf(a, -1.0f, 1.0f);
+                jv = kC09 * jv + kC01 * ak;
+                jp = clipf(jp + jv * kDt, -1.0f, 1.0f);
+            }
+            {
+                const double damp = 1.0 - (fric * 0.1 * 0.01);
+                const float dampf = (float)damp;
+                const bool op32 = (flags & kOpIsF32) != 0, fric_f64 = (flags & kFricF64) != 0;
+                const int ax = s < 3 ? s : 0;
+                const double gz = ax == 2 ? kGz : 0.0, lo = ax == 2 ? 0.0 : -0.2, hi = ax == 2 ? 0.3 : 0.2;
+                float v = fric_f64 ? (float)((double)ovd * damp) : ovd * dampf;
+                v = (float)((double)v + gz);
+                const float inc = v * kDt;
+                double q = op32 ? (double)((float)opd + inc) : opd + (double)inc;
+                q = clipd(q, lo, hi);
+                if ((q <= lo && v < 0.0f) || (q >= hi && v > 0.0f)) v = 0.0f;
+                if (s < 3) {
+                    opd = q;
+                    ovd = v;
+                }
+            }
+            flags &= ~kOpIsF32;
+            const double op3[3] = {gshfl(opd, 0), gshfl(opd, 1), gshfl(opd, 2)};
+            double dmin;
+            float g3[3];
+            const uint32_t c = ls_contacts(jp, op3, size, s, gbit, dmin, g3);
+            // dense_reward (RS:101-187)
+            const double dist = exp(-5.0 * dmin);
+            const double con = (double)__popc(c) / (double)kF;
+            float nacc = 0.0f;  // finger s: sum of its negative joint positions
+#pragma unroll
+            for (int j = 0; j < kJ; ++j)
+                if (g3[j] < 0.0f) nacc = nacc + g3[j];
+            float sum = 0.0f;
+#pragma unroll
+            for (int f = 0; f < kF; ++f) sum = sum + (-gshfl(nacc, f));
+            const float avg = sum / (float)kF;
+            const float clo = clipf(avg / (float)kF, 0.0f, 1.0f);
+            float st = 0.0f;
+            if (flags & kHasPrev) {
+                const uint32_t prev = (flags >> kPrevShift) & 0xFFu;
+                float ch = 0.0f;
+#pragma unroll
+                for (int f = 0; f < kF; ++f) ch = ch + (float)(((c ^ prev) >> f) & 1u);
+                st = clipf(1.0f - ch / (float)kF, 0.0f, 1.0f);
+            }
+            flags = (flags & ~(0xFFu << kPrevShift)) | (c << kPrevShift) | kHasPrev;
+            r = ((p.w.w_dist * dist + p.w.w_con * con) + p.w.w_clo * (double)clo) + p.w.w_st * (double)st;
+            flags = (flags & ~0xFFu) | c;
+            te = __popc(c) >= 3;
+            tr = et >= p.max_episode_steps;
+            et += 1;
+        }
+        ep_ret += r;
+        const bool d = !(p.diag & 2) && (te || tr || et >= p.max_steps);
+        if (s == 0) {
+            p.rew[m] = (float)r;
+            p.done[m] = d;
+        }
+        if (d) {
+            if (s == 0 && cnt < p.record_cap) {
+                const int64_t o = i * p.record_cap + cnt;
+                p.rec_return[o] = ep_ret;
+                p.rec_length[o] = et;
+                p.rec_success[o] = p.success_terminated ? (uint8_t)te : (uint8_t)0;
+                p.rec_end_step[o] = (int32_t)t;
+            }
+            ++cnt;
+            sum_ret += ep_ret;
+            sum_len += et;
+            succ += te;
+            // ---- env_reset_philox, lane-split: lane s draws slot s (joint) and slot 15 + s
+            const dxrl_curriculum& cu = p.s.curricula[cfg];
+            const double u1 = reset_uniform_at(s < kD ? s : 0, ek0, ek1, rctr);
+            const int s2 = s < DXRL_RESET_EXTRA ? s : 0;
+            const double u2 = reset_uniform_at(kD + s2, ek0, ek1, rctr);
+            double v2;
+            if (s2 == 0) v2 = cu.has_size_range ? cu.size_range[0] + (cu.size_range[1] - cu.size_range[0]) * u2 : cu.object_size;
+            else if (s2 == 1) v2 = cu.has_mass_range ? cu.mass_range[0] + (cu.mass_range[1] - cu.mass_range[0]) * u2 : cu.object_mass;
+            else if (s2 == 2)
+                v2 = cu.has_friction_range ? cu.friction_range[0] + (cu.friction_range[1] - cu.friction_range[0]) * u2
+                                           : cu.friction_coefficient;
+            else {
+                const double* rg = s2 == 3 ? cu.spawn_x_range : (s2 == 4 ? cu.spawn_y_range : cu.spawn_z_range);
+                v2 = rg[0] + (rg[1] - rg[0]) * u2;
+            }
+            if (s < kD) {
+                jp = (float)(-0.1 + (0.1 - -0.1) * u1);
+                jv = 0.0f;
+            }
+            size = gshfl(v2, 0);
+            mass = gshfl(v2, 1);
+            fric = gshfl(v2, 2);
+            const double spawn = gshfl(v2, 3 + (s < 3 ? s : 0));
+            const bool has = (flags & kHasObject) != 0;
+            if (s < 3) {
+                opd = (double)(float)(has ? opd : spawn);
+                ovd = 0.0f;
+            }
+            et = 0;
+            flags = kOpIsF32 | kHasObject | (cu.friction_is_f64_scalar ? kFricF64 : 0u);
+            const double op3[3] = {gshfl(opd, 0), gshfl(opd, 1), gshfl(opd, 2)};
+            double dmin;
+            float g3[3];
+            flags |= ls_contacts(jp, op3, size, s, gbit, dmin, g3);
+            ++rctr;
+            ep_ret = 0.0;
+        }
+    }
+    if (live) {
+        // bootstrap observation (slot T), then the state back to the slab
+        write_obs_row(p.iteration * (uint64_t)T + (uint64_t)T);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        tape_obs_row(T * n + i);
+        if (s < kD) {
+            p.s.jp[(int64_t)s * n + i] = jp;
+            p.s.jv[(int64_t)s * n + i] = jv;
+        }
+        if (s < 3) {
+            p.s.op[(int64_t)s * n + i] = opd;
+            p.s.ov[(int64_t)s * n + i] = ovd;
+        }
+        if (s == 0) {
+            p.s.flags[i] = flags;
+            p.s.t[i] = et;
+            p.s.size[i] = size;
+            p.s.mass[i] = mass;
+            p.s.fric[i] = fric;
+            p.s.reset_ctr[i] = rctr;
+            p.ep_ret[i] = ep_ret;
+            p.ep_count[i] = cnt;
+            p.ep_sum_ret[i] = sum_ret;
+            p.ep_sum_len[i] = sum_len;
+            p.ep_succ[i] = succ;
+        }
     }
 }
 
@@ -670,9 +1021,14 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                     a->rec_end_step};
     DeviceGuard g(env->device);
     const int64_t n = env->cfg.num_envs;
-    hipLaunchKernelGGL(k_pg_rollout, dim3((unsigned)((n + kTile - 1) / kTile)), dim3(64 * kRolloutWaves), 0,
+    if (a->obs_fm || (a->diag_flags & 16)) {  // feature-major tape / A-B reference: the 64-env kernel
+        hipLaunchKernelGGL(k_pg_rollout, dim3((unsigned)((n + kTile - 1) / kTile)), dim3(64 * kRolloutWaves), 0,
+                           as_stream(stream), p);
+        return launch_check("k_pg_rollout");
+    }
+    hipLaunchKernelGGL(k_pg_rollout_ls, dim3((unsigned)((n + kLsEnvs - 1) / kLsEnvs)), dim3(64 * kRolloutWaves), 0,
                        as_stream(stream), p);
-    return launch_check("k_pg_rollout");
+    return launch_check("k_pg_rollout_ls");
 }
 
 int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const float* values, int64_t num_envs,

@@ -277,3 +277,30 @@ def test_fused_dynamics_noise(pkg, std):
         inner = res[(np.abs(applied) < 0.999) & (np.abs(policy) < 0.8)]
         assert inner.size > 500
         assert abs(inner.mean()) < 4e-3 and 0.046 < inner.std() < 0.054
+
+
+@pytest.mark.parametrize("cur,n,noise", [("easy", 96, 0.0), ("variable", 100, 0.0), ("hard", 64, 0.05),
+                                         ("variable", 4100, 0.05)])
+def test_lane_split_rollout_matches_64_env_kernel(pkg, cur, n, noise):
+    """k_pg_rollout_ls (16 envs x 16 lanes per workgroup) and k_pg_rollout (one lane per env)
+    share every Philox stream and every op: tapes, episode records and env state are equal bit
+    for bit (including auto-resets, observation / dynamics noise and a ragged last workgroup)."""
+    T = 24
+    outs = []
+    for diag in (16, 0):
+        env = pkg.envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.named(cur), reward_type="dense", seed=11)
+        cfg = pkg.trainer.TrainerConfig(horizon=T, seed=5, max_steps=13, record_cap=T, obs_noise_std=noise,
+                                        dyn_noise_std=noise)
+        tr = pkg.trainer.PGTrainer(env, cfg)
+        env.reset(write_obs=False)
+        tr.diag_flags = diag
+        for _ in range(2):
+            tr.rollout()
+            tr.iteration_index += 1
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (tr.obs_rm, tr.act, tr.logp, tr.rew, tr.done, tr.ep_ret, tr.ep_count,
+                                          tr.rec_return, tr.rec_length, tr.rec_end, env.joint_positions,
+                                          env.joint_velocities, env.object_position, env.object_velocity, env.flags,
+                                          env.step_count, env.object_size, env.friction_coefficient)])
+    for k, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), k

@@ -325,6 +325,99 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16(WgradArgs w) {
     }
 }
 
+// ------------------------------------------------------------------ whole-output weight gradient
+// k_wgrad_full: C[O][I] = sum_m Y[m][o] X[m][i] for O <= 256, I <= 288 (the learner's
+// dW2 = dH2^T [H1 | 1]).  Every workgroup owns a contiguous range of samples and the WHOLE
+// output (8 waves x 32 output rows x 9 column tiles = 144 accumulator registers per lane), so
+// each activation row is read from HBM exactly once -- the tiled k_wgrad_bf16 re-reads Y once
+// per column tile and X once per row tile (2.5x the bytes).  64-sample chunks are staged
+// through two LDS buffers (rows of 576 B: conflict-free transposed reads) with the next chunk's
+// global loads in flight during the current chunk's MFMAs.  Partials [grid][O][I] are summed
+// in block order by k_splitk_reduce.
+constexpr int kFO = 256, kFI = 288, kFK = 64, kFPitch = 288;
+
+__global__ __launch_bounds__(512, 1) void k_wgrad_full(WgradArgs w) {
+    extern __shared__ __attribute__((aligned(16))) bf16 fsm[];
+    const auto Ys = [&](int b) { return fsm + b * kFK * kFPitch; };
+    const auto Xs = [&](int b) { return fsm + (2 + b) * kFK * kFPitch; };
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t mb = (int64_t)blockIdx.x * w.m_chunk;
+    const int64_t me = min(w.M, mb + w.m_chunk);
+    const bool wave_live = 32 * wave < w.O;
+    f32x16 acc[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[j][q] = 0.0f;
+    // chunk = 64 rows x (32 Y + 36 X) 16-byte pieces = 4352 pieces, <= 9 per thread
+    constexpr int kPieces = kFK * (kFO / 8 + kFI / 8), kPer = (kPieces + 511) / 512;
+    bf16x8 pre[kPer];
+    auto fetch = [&](int64_t m0) {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int c = tid + 512 * u;
+            bf16x8 v = zero8();
+            if (c < kPieces) {
+                const bool isy = c < kFK * (kFO / 8);
+                const int cc = isy ? c : c - kFK * (kFO / 8);
+                const int per = isy ? kFO / 8 : kFI / 8;
+                const int row = cc / per, col = 8 * (cc % per);
+                const int64_t m = m0 + row;
+                if (m < me && col < (isy ? w.O : w.I))
+                    v = *reinterpret_cast<const bf16x8*>(isy ? w.Y + m * w.ldy + col : w.X + m * w.ldx + col);
+            }
+            pre[u] = v;
+        }
+    };
+    auto stash = [&](int b) {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int c = tid + 512 * u;
+            if (c < kPieces) {
+                const bool isy = c < kFK * (kFO / 8);
+                const int cc = isy ? c : c - kFK * (kFO / 8);
+                const int per = isy ? kFO / 8 : kFI / 8;
+                const int row = cc / per, col = 8 * (cc % per);
+                *reinterpret_cast<bf16x8*>((isy ? Ys(b) : Xs(b)) + row * kFPitch + col) = pre[u];
+            }
+        }
+    };
+    int b = 0;
+    if (mb < me) {
+        fetch(mb);
+        stash(0);
+    }
+    __syncthreads();
+    for (int64_t m0 = mb; m0 < me; m0 += kFK) {
+        const bool more = m0 + kFK < me;
+        if (more) fetch(m0 + kFK);
+#pragma unroll
+        for (int kk = 0; kk < kFK; kk += 16) {
+            const bf16x8 a = tr_frag<kFPitch>(Ys(b), 32 * wave, kk, lane);
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                const bf16x8 bb = tr_frag<kFPitch>(Xs(b), 32 * j, kk, lane);
+                if (wave_live) acc[j] = mfma32(a, bb, acc[j]);
+            }
+        }
+        if (more) stash(b ^ 1);
+        __syncthreads();
+        b ^= 1;
+    }
+    if (!wave_live) return;
+    float* dst = w.partial ? w.partial + (int64_t)blockIdx.x * w.O * w.I : w.out;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        const int i = 32 * j + (lane & 31);
+        if (i >= w.I) continue;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int o = 32 * wave + acc_row(q, lane);
+            if (o < w.O) dst[(int64_t)o * w.I + i] = acc[j][q];
+        }
+    }
+}
+
 // out[i] (+)= sum_z partial[z][i], fixed order (deterministic)
 __global__ void k_splitk_reduce(const float* __restrict__ partial, int64_t slab, int z, float* __restrict__ out,
                                 int accumulate) {
@@ -333,6 +426,31 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int64_t slab,
     float s = 0.0f;
     for (int k = 0; k < z; ++k) s += partial[(int64_t)k * slab + i];
     out[i] = accumulate ? out[i] + s : s;
+}
+
+// First level of a two-level slab sum: tmp[g][i] = sum of slabs g*z/G .. (g+1)*z/G - 1 (in order),
+// grid.y = G groups, so G x more loads are in flight than in a one-level sum over z slabs.
+__global__ void k_slab_group_sum(const float* __restrict__ partial, int64_t slab, int z, float* __restrict__ tmp) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= slab) return;
+    const int G = gridDim.y, g = blockIdx.y;
+    const int k0 = (int)((int64_t)g * z / G), k1 = (int)((int64_t)(g + 1) * z / G);
+    float s = 0.0f;
+    for (int k = k0; k < k1; ++k) s += partial[(int64_t)k * slab + i];
+    tmp[(int64_t)g * slab + i] = s;
+}
+
+int launch_slab_reduce(const float* partial, int64_t slab, int z, float* tmp, float* out, int accumulate,
+                       hipStream_t st) {
+    const unsigned nb = (unsigned)((slab + 255) / 256);
+    if (z > kReduceGroups && tmp) {
+        hipLaunchKernelGGL(k_slab_group_sum, dim3(nb, kReduceGroups), dim3(256), 0, st, partial, slab, z, tmp);
+        if (int rc = launch_check("k_slab_group_sum")) return rc;
+        partial = tmp;
+        z = kReduceGroups;
+    }
+    hipLaunchKernelGGL(k_splitk_reduce, dim3(nb), dim3(256), 0, st, partial, slab, z, out, accumulate);
+    return launch_check("k_splitk_reduce");
 }
 
 int launch_gemm(const GemmArgs& g0, int splits, float* reduce_out, int accumulate, hipStream_t st) {
@@ -358,9 +476,9 @@ int launch_gemm(const GemmArgs& g0, int splits, float* reduce_out, int accumulat
     if (int rc = launch_check("k_gemm_bf16")) return rc;
     if (g.partial) {
         const int64_t slab = g.M * (int64_t)g.N;
-        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, st, g.partial, slab,
-                           splits, reduce_out, accumulate);
-        if (int rc = launch_check("k_splitk_reduce")) return rc;
+        if (int rc = launch_slab_reduce(g.partial, slab, splits, g.partial + (int64_t)splits * slab, reduce_out,
+                                        accumulate, st))
+            return rc;
     }
     return DXRL_OK;
 }
@@ -378,14 +496,26 @@ int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, 
     splits = (int)((M + chunk - 1) / chunk);
     DXRL_REQUIRE(splits == 1 || partial, "wgrad: split-K needs a partial slab");
     WgradArgs w{Y, ldy, X, ldx, O, I, M, chunk, out, splits > 1 ? partial : nullptr};
+    if (O <= kFO && I <= kFI && O > 128 && M >= (int64_t)splits * kFK) {  // whole output per workgroup
+        static bool attr = [] {
+            return hipFuncSetAttribute(reinterpret_cast<const void*>(k_wgrad_full),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kFK * kFPitch * 2) == hipSuccess;
+        }();
+        DXRL_REQUIRE(attr, "wgrad: could not raise the dynamic LDS limit");
+        hipLaunchKernelGGL(k_wgrad_full, dim3((unsigned)splits), dim3(512), 4 * kFK * kFPitch * 2, st, w);
+        if (int rc = launch_check("k_wgrad_full")) return rc;
+        if (splits > 1) {
+            const int64_t slab = (int64_t)O * I;
+            return launch_slab_reduce(partial, slab, splits, partial + (int64_t)splits * slab, out, 0, st);
+        }
+        return DXRL_OK;
+    }
     const dim3 grid((unsigned)((O + kWO - 1) / kWO), (unsigned)((I + kWI - 1) / kWI), (unsigned)splits);
     hipLaunchKernelGGL(k_wgrad_bf16, grid, dim3(256), 0, st, w);
     if (int rc = launch_check("k_wgrad_bf16")) return rc;
     if (splits > 1) {
         const int64_t slab = (int64_t)O * I;
-        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, st, partial, slab,
-                           splits, out, 0);
-        if (int rc = launch_check("k_splitk_reduce")) return rc;
+        if (int rc = launch_slab_reduce(partial, slab, splits, partial + (int64_t)splits * slab, out, 0, st)) return rc;
     }
     return DXRL_OK;
 }

@@ -24,7 +24,7 @@
 // gradients come straight from the row-major tiles through ds_read_b64_tr_b16.
 //
 // Gradients are deterministic: each workgroup owns a fixed tile set and writes
-// its dW1 / dW3 / dlog_std partials once; k_fused_reduce sums them in block order.
+// its dW1 / dW3 / dlog_std partials once; launch_slab_reduce sums them in a fixed order.
 #include "dxrl_gemm.h"
 #include "dxrl_pg.h"
 
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
 #undef STAMP
     if (!p.train) return;
 
-    // ---- workgroup partials (fixed layout; reduced in block order by k_fused_reduce)
+    // ---- workgroup partials (fixed layout; summed in a fixed order by launch_slab_reduce)
     float* part = p.part + (int64_t)blockIdx.x * kPartSize;
 #pragma unroll
     for (int j = 0; j < kNT; ++j)
@@ -521,16 +521,14 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
     }
 }
 
-// grads blocks W1 / W3 (and log_std for the actor) = sum over workgroups, fixed order
-__global__ void k_fused_reduce(const float* __restrict__ part, int nb, float* __restrict__ gW1, float* __restrict__ gW3,
-                               float* __restrict__ gLs, float ent_coef) {
+// grads blocks W1 / W3 (and log_std for the actor) from the workgroup sum (launch_slab_reduce)
+__global__ void k_fused_scatter(const float* __restrict__ sum, float* __restrict__ gW1, float* __restrict__ gW3,
+                                float* __restrict__ gLs, float ent_coef) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= kPartSize) return;
     const int col = (j - kPartW3) % kHx;
-    const bool w3pad = j >= kPartW3 && j < kPartLs && col > kH;  // never written
-    float s = 0.0f;
-    if (!w3pad)
-        for (int b = 0; b < nb; ++b) s += part[(int64_t)b * kPartSize + j];
+    const bool w3pad = j >= kPartW3 && j < kPartLs && col > kH;  // never written by k_pg_fused
+    const float s = w3pad ? 0.0f : sum[j];
     if (j < kPartW3) gW1[j] = s;
     else if (j < kPartLs) gW3[j - kPartW3] = s;
     else if (gLs) {
@@ -629,9 +627,13 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     }
     if (!train) return DXRL_OK;
     float* G = a->grads;
-    hipLaunchKernelGGL(k_fused_reduce, dim3((kPartSize + 255) / 256), dim3(256), 0, st, a->partial, grid,
+    // the pad columns 257..287 of the W3 slab are never written: the scatter zeroes them
+    float* tmp = a->partial + (int64_t)grid * kPartSize;
+    float* sum = tmp + (int64_t)kReduceGroups * kPartSize;
+    if (int rc = launch_slab_reduce(a->partial, kPartSize, grid, tmp, sum, 0, st)) return rc;
+    hipLaunchKernelGGL(k_fused_scatter, dim3((kPartSize + 255) / 256), dim3(256), 0, st, sum,
                        G + (c ? kOffW1c : kOffW1a), G + o3, c ? nullptr : G + kOffLogStd, (float)a->ent_coef);
-    if (int rc = launch_check("k_fused_reduce")) return rc;
+    if (int rc = launch_check("k_fused_scatter")) return rc;
     // dW2 = dH2^T [H1 | 1]: bias gradient lands in column 256
     return launch_wgrad(static_cast<const bf16*>(a->dh2), kH, kH, static_cast<const bf16*>(a->h1), kHx, kHx, a->rows,
                         a->wgrad_splits, a->wgrad_partial, G + o2, st);

@@ -197,7 +197,8 @@ int dxrl_rollout_simple(dxrl_env* env, void* learner_state, const dxrl_learner_c
  * bias (bias[n*bias_stride]), act (0 identity / 1 tanh), gate (multiply by
  * 1 - gate[m][n]^2), outputs f32 row-major Cf, bf16 row-major Crm, bf16
  * feature-major Cfm[n][m] (each nullable).  splits > 1: split-K over K into
- * `partial` (f32 [splits][M][N]) reduced into Cf (ld = N).  K % 32 == 0.
+ * `partial` (f32 [splits + 16][M][N]: the last 16 slabs are the two-level reduction's
+ * scratch) reduced into Cf (ld = N).  K % 32 == 0.
  * ------------------------------------------------------------------------ */
 int dxrl_gemm_bf16(int32_t device, const void* A, int64_t lda, const void* Bt, int64_t ldb, int64_t M, int32_t N,
                    int32_t K, const float* bias, int64_t bias_stride, int32_t act, const void* gate, int64_t ldg,
@@ -205,7 +206,8 @@ int dxrl_gemm_bf16(int32_t device, const void* A, int64_t lda, const void* Bt, i
                    int64_t ldffm, int32_t splits, float* partial, void* stream);
 /* Weight gradient out[O][I] = sum_m Y[m][o] X[m][i] from row-major bf16 operands
  * (k-major MFMA operands via ds_read_b64_tr_b16); split-K over m into `partial`
- * (f32 [splits][O][I]) reduced in fixed order (deterministic).  O, I, ldy, ldx % 8 == 0. */
+ * (f32 [splits + 16][O][I]; the last 16 slabs are reduction scratch) reduced in fixed order
+ * (deterministic).  O, I, ldy, ldx % 8 == 0. */
 int dxrl_wgrad_bf16(int32_t device, const void* Y, int64_t ldy, int32_t O, const void* X, int64_t ldx, int32_t I,
                     int64_t M, int32_t splits, float* partial, float* out, void* stream);
 
@@ -315,11 +317,11 @@ typedef struct dxrl_pg_fused_args {
     float* values;             /* forward mode: f32 [rows]                                 */
     void* h1;                  /* bf16 [rows][288] scratch, column 256 preset to 1         */
     void* dh2;                 /* bf16 [rows][256] scratch                                 */
-    float* partial;            /* f32 [grid][dxrl_pg_fused_sizes().partial_floats]         */
+    float* partial;            /* f32 [grid + 17][dxrl_pg_fused_sizes().partial_floats]    */
     double* loss_partial;      /* f64 [grid][4]: actor writes 0,2,3, critic writes 1       */
     int32_t grid;              /* workgroups (one per CU: 256 on MI355X)                   */
     int32_t wgrad_splits;      /* split-K factor of the dW2 GEMM                           */
-    float* wgrad_partial;      /* f32 [wgrad_splits][256][288]                             */
+    float* wgrad_partial;      /* f32 [wgrad_splits + 16][256][288]                        */
     float* grads;              /* f32 master-layout gradients: W1/W2/W3 (+ log_std) blocks */
 } dxrl_pg_fused_args;
 

@@ -25,7 +25,7 @@ def gemm(N, A, Bt, *, bias=None, bias_stride=1, act=0, gate=None, out_f32=True, 
     Cf = torch.zeros(M, Nn, dtype=torch.float32, device=dev) if out_f32 else None
     Crm = torch.zeros(M, Nn, dtype=torch.bfloat16, device=dev) if out_rm else None
     Cfm = torch.zeros(Nn, M, dtype=torch.bfloat16, device=dev) if out_fm else None
-    partial = torch.empty(splits, M, Nn, dtype=torch.float32, device=dev) if splits > 1 else None
+    partial = torch.empty(splits + 16, M, Nn, dtype=torch.float32, device=dev) if splits > 1 else None
     p = N.ptr
     N.call("dxrl_gemm_bf16", dev.index, p(A), A.stride(0), p(Bt), Bt.stride(0), M, Nn, K, p(bias), bias_stride, act,
            p(gate), 0 if gate is None else gate.stride(0), p(Cf), Nn, p(Crm), Nn, p(Cfm), M, None, 0, splits, p(partial),
@@ -86,7 +86,7 @@ def wgrad(N, Y, O, X, I, splits=1):
     M = Y.shape[0]
     dev = Y.device
     out = torch.full((O, I), float("nan"), dtype=torch.float32, device=dev)
-    partial = torch.empty(max(splits, 1), O, I, dtype=torch.float32, device=dev)
+    partial = torch.empty(max(splits, 1) + 16, O, I, dtype=torch.float32, device=dev)
     p = N.ptr
     N.call("dxrl_wgrad_bf16", dev.index, p(Y), Y.stride(0), O, p(X), X.stride(0), I, M, splits, p(partial), p(out),
            N.stream_of(dev))
@@ -96,7 +96,8 @@ def wgrad(N, Y, O, X, I, splits=1):
 
 @pytest.mark.parametrize("M,O,ldy,I,ldx,splits", [(64, 128, 128, 128, 128, 1), (1000, 256, 256, 288, 288, 1),
                                                   (4096, 32, 32, 288, 288, 7), (3232, 256, 256, 64, 64, 5),
-                                                  (50016, 256, 256, 288, 288, 33)])
+                                                  (50016, 256, 256, 288, 288, 33), (1000, 200, 256, 264, 288, 4),
+                                                  (819200, 256, 256, 288, 288, 256)])
 def test_wgrad_transposed_lds_reads(N, M, O, ldy, I, ldx, splits):
     """out[o][i] = sum_m Y[m][o] X[m][i] from row-major operands (ds_read_b64_tr_b16 path)."""
     g = torch.Generator(device="cuda").manual_seed(M + O + I)
@@ -105,6 +106,16 @@ def test_wgrad_transposed_lds_reads(N, M, O, ldy, I, ldx, splits):
     out = wgrad(N, Y, O, X, I, splits)
     ref = Y[:, :O].float().T @ X[:, :I].float()
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3 * (M / 1000) ** 0.5)
+
+
+@pytest.mark.parametrize("M,O,I,splits", [(700, 256, 288, 3), (4160, 136, 200, 5)])
+def test_wgrad_full_output_exact_integer(N, M, O, I, splits):
+    """The whole-output kernel (k_wgrad_full: O > 128) on exact small integers, ragged M chunks."""
+    Y = (torch.arange(M * O, device="cuda").reshape(M, O) % 7 - 3).to(torch.bfloat16)
+    X = (torch.arange(M * I, device="cuda").reshape(M, I) % 5 - 2).float().mul(torch.arange(I, device="cuda") % 3 + 1)
+    X = X.to(torch.bfloat16)
+    out = wgrad(N, Y, O, X, I, splits)
+    assert torch.equal(out, Y.float().T @ X.float())
 
 
 def test_wgrad_exact_integer_asymmetric(N):

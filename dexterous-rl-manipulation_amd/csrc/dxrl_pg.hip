@@ -13,6 +13,10 @@
 #include "dxrl_gemm.h"
 #include "dxrl_pg.h"
 
+#include <stdio.h>
+
+#include <vector>
+
 using namespace dxrl;
 using namespace dxrl::pg;
 
@@ -75,6 +79,7 @@ struct PgRolloutArgs {
     int32_t* rec_length;
     uint8_t* rec_success;
     int32_t* rec_end_step;
+    unsigned long long* stamps;  // diag & 32 (k_pg_rollout_ls): cycles per step segment
 };
 
 constexpr int kTile = 64;           // envs per workgroup
@@ -162,16 +167,28 @@ __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfr
         for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.0f;
+    if constexpr (RT == 1) {
+        // one row tile: issue every activation fragment up front (KS LDS reads in flight),
+        // then the MFMA chain consumes them with counted waits
+        bf16x8 a[KS];
 #pragma unroll
-    for (int k = 0; k < KS; ++k) {
-        bf16x8 a[RT];
+        for (int k = 0; k < KS; ++k) a[k] = *reinterpret_cast<const bf16x8*>(A + r * lda + 16 * k + 8 * h);
 #pragma unroll
-        for (int i = 0; i < RT; ++i) a[i] = *reinterpret_cast<const bf16x8*>(A + (32 * i + r) * lda + 16 * k + 8 * h);
+        for (int k = 0; k < KS; ++k)
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            const bf16x8 b = wfrag(j, k);
+            for (int j = 0; j < NT; ++j) acc[0][j] = mfma32(a[k], wfrag(j, k), acc[0][j]);
+    } else {
 #pragma unroll
-            for (int i = 0; i < RT; ++i) acc[i][j] = mfma32(a[i], b, acc[i][j]);
+        for (int k = 0; k < KS; ++k) {
+            bf16x8 a[RT];
+#pragma unroll
+            for (int i = 0; i < RT; ++i) a[i] = *reinterpret_cast<const bf16x8*>(A + (32 * i + r) * lda + 16 * k + 8 * h);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const bf16x8 b = wfrag(j, k);
+#pragma unroll
+                for (int i = 0; i < RT; ++i) acc[i][j] = mfma32(a[i], b, acc[i][j]);
+            }
         }
     }
 #pragma unroll
@@ -361,20 +378,10 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout(PgRolloutA
 // over 16 lanes of one wave: lane s owns joint s (jp, jv), lanes 0..2 the object's axis s,
 // and every lane keeps a copy of the env's scalars (flags, step, size, mass, friction ...).
 // Elementwise physics runs lane-parallel; the reference's ordered sums (finger sums, the
-// closure term, log pi) are gathered with in-group shuffles and added in the reference order
+// closure term, log pi) are gathered through a per-env LDS row and added in the reference order
 // on every lane.  The actor MLP runs on all four waves as in k_pg_rollout, on one 32-row
 // MFMA tile of which rows 0..15 are this workgroup's envs.
 constexpr int kLsEnvs = 16, kLsLanes = 16;
-
-template <typename T>
-__device__ __forceinline__ T gshfl(T v, int src) {  // value of lane `src` of this 16-lane group
-    return __shfl(v, src, kLsLanes);
-}
-__device__ __forceinline__ double gshfl(double v, int src) {
-    const int2 b = *reinterpret_cast<int2*>(&v);
-    const int2 r{__shfl(b.x, src, kLsLanes), __shfl(b.y, src, kLsLanes)};
-    return *reinterpret_cast<const double*>(&r);
-}
 
 // standard normal k of Philox block k / 4 (Box-Muller pairs (x, y), (z, w)), as philox_normals
 __device__ __forceinline__ float philox_normal_at(int k, uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream) {
@@ -391,13 +398,24 @@ __device__ __forceinline__ double reset_uniform_at(int k, uint32_t k0, uint32_t 
     return (k & 1) ? u01_53(r.z, r.w) : u01_53(r.x, r.y);
 }
 
+// In-group exchange through a per-env LDS row (dwords): one LDS write + wide reads replace a
+// chain of ds_bpermute shuffles.  All 16 lanes of a group are in one wave, so a wavefront-scope
+// fence (compiler ordering + lgkmcnt) is the only synchronisation needed.
+constexpr int kGx = 72, kGxJp = 0, kGxTerm = 16, kGxNacc = 32, kGxD = 40, kGxOp = 50, kGxV2 = 56;
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Lane-split contacts_of: every lane of the group gets the mask and the minimum distance.
-// gbit: this group's bit offset in the wave's ballot.
+// gbit: this group's bit offset in the wave's ballot; op: the object position (all lanes).
 __device__ __forceinline__ uint32_t ls_contacts(float jp, const double op[3], double size, int s, int gbit,
-                                                double& dmin, float g3[3]) {
+                                                double& dmin, float g3[3], float* gx) {
+    gx[kGxJp + s] = jp;
+    wsync();
     const int f = s < kF ? s : 0;
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) g3[j] = gshfl(jp, kJ * f + j);
+    for (int j = 0; j < kJ; ++j) g3[j] = gx[kGxJp + kJ * f + j];
     float sum = g3[0];
 #pragma unroll
     for (int j = 1; j < kJ; ++j) sum = sum + g3[j];
@@ -406,13 +424,25 @@ __device__ __forceinline__ uint32_t ls_contacts(float jp, const double op[3], do
     const double d = sqrt((dx * dx + dy * dy) + dz * dz);
     const bool hit = s < kF && d < size * 1.5;
     const uint32_t mask = (uint32_t)(__ballot(hit) >> gbit) & ((1u << kF) - 1u);
-    dmin = gshfl(d, 0);
+    double* gd = reinterpret_cast<double*>(gx + kGxD);
+    if (s < kF) gd[s] = d;
+    wsync();
+    dmin = gd[0];
 #pragma unroll
     for (int k = 1; k < kF; ++k) {
-        const double dk = gshfl(d, k);
+        const double dk = gd[k];
         dmin = dk < dmin ? dk : dmin;
     }
     return mask;
+}
+
+// the object position from lanes 0..2 to every lane of the group
+__device__ __forceinline__ void ls_object(double opd, int s, double op[3], float* gx) {
+    double* go = reinterpret_cast<double*>(gx + kGxOp);
+    if (s < 3) go[s] = opd;
+    wsync();
+#pragma unroll
+    for (int d = 0; d < 3; ++d) op[d] = go[d];
 }
 
 __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRolloutArgs p) {
@@ -424,8 +454,10 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
     __shared__ __attribute__((aligned(16))) bf16 H2[kRows * kHs];
     __shared__ float MU[kLsEnvs * (kOut + 1)];
     __shared__ float LS[kActPad], SIG[kActPad], ISIG[kActPad];
+    __shared__ __attribute__((aligned(16))) float GX[kLsEnvs * kGx];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int eg = tid >> 4, s = tid & 15, gbit = 16 * (eg & 3);
+    float* gx = GX + eg * kGx;
     const int64_t n = p.s.n;
     const int64_t i = (int64_t)blockIdx.x * kLsEnvs + eg;
     const bool live = i < n;
@@ -439,6 +471,8 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
     WTile<kH / 16> w2[kNT];
 #pragma unroll
     for (int j = 0; j < kNT; ++j) load_wtile(w2[j], p.wbf + kBfW2a, kHx, kCpw * wave + 32 * j, lane);
+    WTile<kH / 16> w3r;  // the mu wave's W3 fragments (rows = head outputs)
+    if (wave == kRolloutWaves - 1) load_wtile(w3r, p.wbf + kBfW3a, kHx, 0, lane);
     for (int c = tid; c < kH * (kIn / 8); c += 64 * kRolloutWaves) {
         const int row = c / (kIn / 8), col = 8 * (c % (kIn / 8));
         *reinterpret_cast<bf16x8*>(W1s + row * kW1s + col) =
@@ -494,6 +528,22 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
         env_key(p.env_seed, p.gid0 + i, ek0, ek1);
         env_key(p.policy_seed, p.gid0 + i, pk0, pk1);
     }
+    // this lane's reset slot 15 + s2 of the env's curriculum row (the row is fixed for the launch)
+    const int s2 = s < DXRL_RESET_EXTRA ? s : 0;
+    double lo2 = 0.0, hi2 = 0.0, cst2 = 0.0;
+    bool has2 = true, fric64 = false;
+    if (live) {
+        const dxrl_curriculum& cu = p.s.curricula[cfg];
+        const double* rg = s2 == 0 ? cu.size_range
+                                   : s2 == 1 ? cu.mass_range
+                                             : s2 == 2 ? cu.friction_range
+                                                       : s2 == 3 ? cu.spawn_x_range : s2 == 4 ? cu.spawn_y_range : cu.spawn_z_range;
+        lo2 = rg[0];
+        hi2 = rg[1];
+        cst2 = s2 == 0 ? cu.object_size : s2 == 1 ? cu.object_mass : cu.friction_coefficient;
+        has2 = s2 == 0 ? cu.has_size_range != 0 : s2 == 1 ? cu.has_mass_range != 0 : s2 == 2 ? cu.has_friction_range != 0 : true;
+        fric64 = cu.friction_is_f64_scalar != 0;
+    }
     // observation row of this env (+ observation noise): lane s writes jp[s], jv[s], the
     // object axis s, a quaternion slot and a contact bit -- element k of ME:254-264
     const auto write_obs_row = [&](uint64_t ctr) {
@@ -519,32 +569,50 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
         *reinterpret_cast<bf16x4*>(p.obs_rm + m * kIn + 4 * s) = *reinterpret_cast<const bf16x4*>(X + eg * kXs + 4 * s);
     };
     const bool mlp = !(p.diag & 1);
+    unsigned long long st_acc[8], st_last = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) st_acc[k] = 0;
+#define LS_STAMP(k)                                                                              \
+    do {                                                                                         \
+        if (p.diag & 32) {                                                                       \
+            __builtin_amdgcn_sched_barrier(0);                                                   \
+            unsigned long long t_;                                                               \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+            __builtin_amdgcn_sched_barrier(0);                                                   \
+            st_acc[k] += t_ - st_last;                                                           \
+            st_last = t_;                                                                        \
+        }                                                                                        \
+    } while (0)
+    LS_STAMP(7);
     for (int64_t t = 0; t < T; ++t) {
         const int64_t m = t * n + i;
         const uint64_t ctr = p.iteration * (uint64_t)T + (uint64_t)t;
         if (live) write_obs_row(ctr);
+        LS_STAMP(0);
         __syncthreads();
         if (live) tape_obs_row(m);
         if (mlp) wave_layer<kIn / 16, kNT, true, 1>(X, kXs, w1frag, kCpw * wave, nullptr, 0, H1, kHs, lane);
         __syncthreads();
+        LS_STAMP(1);
         if (mlp) wave_layer<kH / 16, kNT, true, 1>(H1, kHs, w2frag, kCpw * wave, p.params + kOffW2a + kH, kHx, H2,
                                                   kHs, lane);
         __syncthreads();
+        LS_STAMP(2);
         if (mlp && wave == kRolloutWaves - 1) {  // mu head: 16 env rows x 32 head rows
             f32x16 acc;
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+            bf16x8 ah[kH / 16];
 #pragma unroll
-            for (int k = 0; k < kH / 16; ++k) {
-                const bf16x8 a = *reinterpret_cast<const bf16x8*>(H2 + r32 * kHs + 16 * k + 8 * h2);
-                const bf16x8 b = *reinterpret_cast<const bf16x8*>(W3s + r32 * kW3s + 16 * k + 8 * h2);
-                acc = mfma32(a, b, acc);
-            }
+            for (int k = 0; k < kH / 16; ++k) ah[k] = *reinterpret_cast<const bf16x8*>(H2 + r32 * kHs + 16 * k + 8 * h2);
+#pragma unroll
+            for (int k = 0; k < kH / 16; ++k) acc = mfma32(ah[k], w3r.b[k], acc);
             const float bias = p.params[kOffW3a + (int64_t)r32 * kHx + kH];
 #pragma unroll
             for (int q = 0; q < 8; ++q) MU[acc_row(q, lane) * (kOut + 1) + r32] = acc[q] + bias;  // rows < 16
         }
         __syncthreads();
+        LS_STAMP(3);
         if (!live) continue;
         // ---- a = mu + sigma * eps, log pi(a|s) in action order (gauss_logp's order)
         const int sa = s < kAct ? s : 0;
@@ -552,13 +620,22 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
         float a = mu + SIG[sa] * philox_normal_at(sa, pk0, pk1, ctr, kStreamPolicy);
         const float z = (a - mu) * ISIG[sa];
         const float term = -0.5f * z * z - LS[sa] - 0.5f * kLog2Pi;
+        gx[kGxTerm + s] = term;
+        wsync();
         float lp = 0.0f;
 #pragma unroll
-        for (int k = 0; k < kAct; ++k) lp += gshfl(term, k);
+        for (int q = 0; q < 4; ++q) {
+            const float4 t4 = reinterpret_cast<const float4*>(gx + kGxTerm)[q];
+            lp += t4.x;
+            lp += t4.y;
+            lp += t4.z;
+            if (4 * q + 3 < kAct) lp += t4.w;
+        }
         p.act[m * kActPad + s] = s < kAct ? a : 0.0f;
         if (s == 0) p.logp[m] = lp;
         if (p.dyn_noise > 0.0f)  // robustness_tests.py:180-187 (the tape keeps the policy's action)
             a = clipf(a + p.dyn_noise * philox_normal_at(sa, pk0, pk1, ctr, kStreamDyn), -1.0f, 1.0f);
+        LS_STAMP(4);
         bool te = false, tr = false;
         double r = 0.0;
         if (!(p.diag & 2)) {
@@ -586,10 +663,11 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
                 }
             }
             flags &= ~kOpIsF32;
-            const double op3[3] = {gshfl(opd, 0), gshfl(opd, 1), gshfl(opd, 2)};
+            double op3[3];
+            ls_object(opd, s, op3, gx);
             double dmin;
             float g3[3];
-            const uint32_t c = ls_contacts(jp, op3, size, s, gbit, dmin, g3);
+            const uint32_t c = ls_contacts(jp, op3, size, s, gbit, dmin, g3, gx);
             // dense_reward (RS:101-187)
             const double dist = exp(-5.0 * dmin);
             const double con = (double)__popc(c) / (double)kF;
@@ -597,9 +675,11 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
 #pragma unroll
             for (int j = 0; j < kJ; ++j)
                 if (g3[j] < 0.0f) nacc = nacc + g3[j];
+            if (s < kF) gx[kGxNacc + s] = nacc;
+            wsync();
             float sum = 0.0f;
 #pragma unroll
-            for (int f = 0; f < kF; ++f) sum = sum + (-gshfl(nacc, f));
+            for (int f = 0; f < kF; ++f) sum = sum + (-gx[kGxNacc + f]);
             const float avg = sum / (float)kF;
             const float clo = clipf(avg / (float)kF, 0.0f, 1.0f);
             float st = 0.0f;
@@ -617,6 +697,7 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
             tr = et >= p.max_episode_steps;
             et += 1;
         }
+        LS_STAMP(5);
         ep_ret += r;
         const bool d = !(p.diag & 2) && (te || tr || et >= p.max_steps);
         if (s == 0) {
@@ -636,43 +717,42 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
             sum_len += et;
             succ += te;
             // ---- env_reset_philox, lane-split: lane s draws slot s (joint) and slot 15 + s
-            const dxrl_curriculum& cu = p.s.curricula[cfg];
             const double u1 = reset_uniform_at(s < kD ? s : 0, ek0, ek1, rctr);
-            const int s2 = s < DXRL_RESET_EXTRA ? s : 0;
             const double u2 = reset_uniform_at(kD + s2, ek0, ek1, rctr);
-            double v2;
-            if (s2 == 0) v2 = cu.has_size_range ? cu.size_range[0] + (cu.size_range[1] - cu.size_range[0]) * u2 : cu.object_size;
-            else if (s2 == 1) v2 = cu.has_mass_range ? cu.mass_range[0] + (cu.mass_range[1] - cu.mass_range[0]) * u2 : cu.object_mass;
-            else if (s2 == 2)
-                v2 = cu.has_friction_range ? cu.friction_range[0] + (cu.friction_range[1] - cu.friction_range[0]) * u2
-                                           : cu.friction_coefficient;
-            else {
-                const double* rg = s2 == 3 ? cu.spawn_x_range : (s2 == 4 ? cu.spawn_y_range : cu.spawn_z_range);
-                v2 = rg[0] + (rg[1] - rg[0]) * u2;
-            }
+            const double v2 = has2 ? lo2 + (hi2 - lo2) * u2 : cst2;  // config.py:44-113 samplers
             if (s < kD) {
                 jp = (float)(-0.1 + (0.1 - -0.1) * u1);
                 jv = 0.0f;
             }
-            size = gshfl(v2, 0);
-            mass = gshfl(v2, 1);
-            fric = gshfl(v2, 2);
-            const double spawn = gshfl(v2, 3 + (s < 3 ? s : 0));
+            double* gv = reinterpret_cast<double*>(gx + kGxV2);
+            if (s < DXRL_RESET_EXTRA) gv[s] = v2;
+            wsync();
+            size = gv[0];
+            mass = gv[1];
+            fric = gv[2];
+            const double spawn = gv[3 + (s < 3 ? s : 0)];
             const bool has = (flags & kHasObject) != 0;
             if (s < 3) {
                 opd = (double)(float)(has ? opd : spawn);
                 ovd = 0.0f;
             }
             et = 0;
-            flags = kOpIsF32 | kHasObject | (cu.friction_is_f64_scalar ? kFricF64 : 0u);
-            const double op3[3] = {gshfl(opd, 0), gshfl(opd, 1), gshfl(opd, 2)};
+            flags = kOpIsF32 | kHasObject | (fric64 ? kFricF64 : 0u);
+            double op3[3];
+            ls_object(opd, s, op3, gx);
             double dmin;
             float g3[3];
-            flags |= ls_contacts(jp, op3, size, s, gbit, dmin, g3);
+            flags |= ls_contacts(jp, op3, size, s, gbit, dmin, g3, gx);
             ++rctr;
             ep_ret = 0.0;
         }
+        LS_STAMP(6);
     }
+    if ((p.diag & 32) && s == 0 && live) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p.stamps[i * 8 + k] = st_acc[k];
+    }
+#undef LS_STAMP
     if (live) {
         // bootstrap observation (slot T), then the state back to the slab
         write_obs_row(p.iteration * (uint64_t)T + (uint64_t)T);
@@ -1026,9 +1106,30 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                            as_stream(stream), p);
         return launch_check("k_pg_rollout");
     }
+    static unsigned long long* stamps = nullptr;
+    static int64_t stamps_n = 0;
+    if ((a->diag_flags & 32) && stamps_n < n) {
+        if (stamps) (void)hipFree(stamps);
+        (void)hipMalloc(&stamps, (size_t)n * 8 * sizeof(unsigned long long));
+        stamps_n = n;
+    }
+    p.stamps = stamps;
     hipLaunchKernelGGL(k_pg_rollout_ls, dim3((unsigned)((n + kLsEnvs - 1) / kLsEnvs)), dim3(64 * kRolloutWaves), 0,
                        as_stream(stream), p);
-    return launch_check("k_pg_rollout_ls");
+    if (int rc = launch_check("k_pg_rollout_ls")) return rc;
+    if (a->diag_flags & 32) {  // diagnostic builds: mean cycles per env per step segment
+        std::vector<unsigned long long> h((size_t)n * 8);
+        (void)hipStreamSynchronize(as_stream(stream));
+        (void)hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost);
+        fprintf(stderr, "rollout_ls cycles/step:");
+        for (int k = 0; k < 8; ++k) {
+            double sum = 0;
+            for (int64_t e = 0; e < n; ++e) sum += (double)h[e * 8 + k];
+            fprintf(stderr, " s%d=%.0f", k, sum / n / a->horizon);
+        }
+        fprintf(stderr, "\n");
+    }
+    return DXRL_OK;
 }
 
 int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const float* values, int64_t num_envs,

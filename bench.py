@@ -233,15 +233,14 @@ def step_kernel_roofline(args, dev):
     for _ in range(3):
         env.step(acts)
     torch.cuda.synchronize(dev)
-    stream = torch.cuda.current_stream(dev)
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.roofline_launches + 1)]
-    evs[0].record(stream)
-    for k in range(args.roofline_launches):
+    stream = torch.cuda.current_stream(dev)  # dxrl_env_step launches on this stream
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.roofline_launches):
         env.step(acts)
-        evs[k + 1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
-    per = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.roofline_launches)]
-    ms = float(np.mean(per))
+    ms = ev0.elapsed_time(ev1) / args.roofline_launches  # back-to-back launches, average per launch
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
     if os.path.exists(pmc):

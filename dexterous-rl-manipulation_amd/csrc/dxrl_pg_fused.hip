@@ -195,7 +195,9 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 }
 
 // kFW waves per workgroup: 4 (one per SIMD, 512 registers each) or 8 (two per SIMD)
-template <int kFW>
+// kTrain: forward + heads + backward; otherwise the forward-only critic-value pass, which keeps
+// no launch-long accumulators and so fits two waves per SIMD.
+template <int kFW, bool kTrain>
 __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
     constexpr int kFThreads = 64 * kFW;
     constexpr int kNT = kH / 32 / kFW;  // 32-wide feature tiles per wave
@@ -223,8 +225,8 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
     for (int j = 0; j < 8; ++j) dls[j] = db3[j] = 0.0f;
     double lsum[4] = {0.0, 0.0, 0.0, 0.0};
 
-    const double adv_mean = p.train && p.net == 0 ? p.stats[2] : 0.0;
-    const double adv_div = p.train && p.net == 0 ? p.stats[4] + 1e-8 : 1.0;
+    const double adv_mean = kTrain && p.net == 0 ? p.stats[2] : 0.0;
+    const double adv_div = kTrain && p.net == 0 ? p.stats[4] + 1e-8 : 1.0;
 
     // X tile prefetch: 128 rows x 8 chunks of 16 B = 1024 chunks, 4 per thread
     constexpr int kXU = kTR * (kIn / 8) / kFThreads;
@@ -256,6 +258,13 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
     STAMP(15);
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t m0 = tile * kTR;
+        // lane-derived addresses are recomputed per tile instead of being hoisted out of the
+        // loop by the compiler (dozens of loop-invariant address registers otherwise)
+        int tid_l = (int)threadIdx.x;
+        asm volatile("" : "+v"(tid_l));
+        const int lane = tid_l & 63, r = lane & 31, h = lane >> 5;
+        (void)r;
+        (void)h;
         const bf16 *W1 = opaque(p.W1), *W2 = opaque(p.W2), *W3 = opaque(p.W3), *W2T = opaque(p.W2T),
                    *W3T = opaque(p.W3T);
         const float *b2 = opaque(p.b2), *b3 = opaque(p.b3), *logstd = opaque(p.logstd);
@@ -311,7 +320,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
                 b3v[q] = ((gf32*)b3)[(int64_t)((q & 3) + 8 * (q >> 2) + 4 * h) * kHx];  // head row o of register q
             }
             if (p.net == 0) {
-                if (p.train) {
+                if (kTrain) {
                     float mu[8], a[8], lsv[8], iv2[8];
 #pragma unroll
                     for (int q = 0; q < 8; ++q) {
@@ -378,7 +387,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
                 }
             } else {
                 const float v = acc[0] + b3v[0];  // lanes h == 0 hold head row 0
-                if (!p.train) {
+                if (!kTrain) {
                     if (valid && h == 0) p.v_out[m] = v;
                 } else if (valid && h == 0) {
                     const float e = v - p.ret[m];
@@ -387,7 +396,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
                     lsum[1] += (double)e * (double)e;
                 }
             }
-            if (p.train) {
+            if (kTrain) {
 #pragma unroll
                 for (int g2 = 0; g2 < 4; ++g2) {  // head rows 8 g2 + 4 h .. + 3
                     bf16x4 v;
@@ -398,7 +407,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
             }
         }
         STAMP(6);
-        if (!p.train) {
+        if (!kTrain) {
             if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
             __syncthreads();  // X / H1 / H2 are rewritten by the next tile
             STAMP(7);
@@ -475,7 +484,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
         for (int k = 0; k < 16; ++k) p.stamps[((int64_t)blockIdx.x * kFW + wave) * 16 + k] = st_acc[k];
     }
 #undef STAMP
-    if (!p.train) return;
+    if (!kTrain) return;
 
     // ---- workgroup partials (fixed layout; summed in a fixed order by launch_slab_reduce)
     float* part = p.part + (int64_t)blockIdx.x * kPartSize;
@@ -604,14 +613,15 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     }();
     f.diag = diag;
     static const int waves = [] {
-        const char* v = getenv("DXRL_FUSED_WAVES");
-        return v && atoi(v) == 8 ? 8 : 4;
+        const char* v = getenv("DXRL_FUSED_WAVES");  // A/B: 4 = one wave per SIMD
+        return v && atoi(v) == 4 ? 4 : 8;
     }();
     static unsigned long long* stamps = nullptr;
     if ((diag & 8) && !stamps) (void)hipMalloc(&stamps, (size_t)65536 * 8 * 16 * 8);
     f.stamps = stamps;
-    if (waves == 8) hipLaunchKernelGGL(k_pg_fused<8>, dim3(grid), dim3(512), 0, st, f);
-    else hipLaunchKernelGGL(k_pg_fused<4>, dim3(grid), dim3(256), 0, st, f);
+    if (!train) hipLaunchKernelGGL((k_pg_fused<8, false>), dim3(grid), dim3(512), 0, st, f);
+    else if (waves == 8) hipLaunchKernelGGL((k_pg_fused<8, true>), dim3(grid), dim3(512), 0, st, f);
+    else hipLaunchKernelGGL((k_pg_fused<4, true>), dim3(grid), dim3(256), 0, st, f);
     if (int rc = launch_check("k_pg_fused")) return rc;
     if (diag & 8) {  // print the mean cycles per segment per wave (diagnostic builds only)
         std::vector<unsigned long long> h((size_t)grid * waves * 16);

@@ -15,7 +15,7 @@ import threading
 import torch  # noqa: F401  (loads libamdhip64 first; see module docstring)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libdxrl.so")
+LIB_PATH = os.environ.get("DXRL_LIB") or os.path.join(PKG_DIR, "libdxrl.so")  # DXRL_LIB: A/B builds
 
 DXRL_OK = 0
 DXRL_E_INVALID = -1

@@ -35,11 +35,12 @@ int launch_gemm(const GemmArgs& g, int splits, float* reduce_out, int accumulate
 // out (+)= sum of z slabs of `slab` floats, deterministic; z > kReduceGroups runs two levels through
 // tmp [kReduceGroups][slab] (callers reserve it right after their z partial slabs).
 constexpr int kReduceGroups = 16;
+// cols > 0: the slab is [rows][cols] and lands in out with row stride ldo.
 int launch_slab_reduce(const float* partial, int64_t slab, int z, float* tmp, float* out, int accumulate,
-                       hipStream_t st);
+                       hipStream_t st, int cols = 0, int64_t ldo = 0);
 // out[O][I] = sum_m Y[m][o] X[m][i] (row-major operands, split-K over m; partial holds
 // [splits + kReduceGroups][O][I]).
 int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, int I, int64_t M, int splits,
-                 float* partial, float* out, hipStream_t st);
+                 float* partial, float* out, hipStream_t st, int64_t ldo = 0);
 
 }  // namespace dxrl

@@ -11,6 +11,8 @@
 // row-major operands k-major straight out of LDS with ds_read_b64_tr_b16
 // (gfx950 transpose read, cdna_hip_programming.md T10), so no feature-major
 // copy of any activation is ever written.
+#include <stdlib.h>
+
 #include "dxrl_internal.h"
 #include "dxrl_gemm.h"
 
@@ -247,8 +249,10 @@ struct WgradArgs {
     int64_t ldx;
     int O, I;
     int64_t M, m_chunk;
-    float* out;      // [O][I] f32 (splits == 1)
+    float* out;      // [O][ldo] f32 (splits == 1)
     float* partial;  // [splits][O][I] (splits > 1)
+    int64_t ldo;     // output row stride (>= I)
+    int diag;        // timing ablation (DXRL_WGRAD_DIAG): 1 = stream only, no fragment reads / MFMAs
 };
 
 __global__ __launch_bounds__(256) void k_wgrad_bf16(WgradArgs w) {
@@ -311,6 +315,7 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16(WgradArgs w) {
     }
     if (!wave_live) return;
     float* dst = w.partial ? w.partial + (int64_t)blockIdx.z * w.O * w.I : w.out;
+    const int64_t ld = w.partial ? w.I : w.ldo;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int i = i0 + wi + 32 * j + (lane & 31);
@@ -320,112 +325,260 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16(WgradArgs w) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int o = o0 + wo + 32 * ii + acc_row(q, lane);
-                if (o < w.O) dst[(int64_t)o * w.I + i] = acc[ii][j][q];
+                if (o < w.O) dst[(int64_t)o * ld + i] = acc[ii][j][q];
             }
     }
 }
 
 // ------------------------------------------------------------------ whole-output weight gradient
-// k_wgrad_full: C[O][I] = sum_m Y[m][o] X[m][i] for O <= 256, I <= 288 (the learner's
-// dW2 = dH2^T [H1 | 1]).  Every workgroup owns a contiguous range of samples and the WHOLE
-// output (8 waves x 32 output rows x 9 column tiles = 144 accumulator registers per lane), so
-// each activation row is read from HBM exactly once -- the tiled k_wgrad_bf16 re-reads Y once
-// per column tile and X once per row tile (2.5x the bytes).  64-sample chunks are staged
-// through two LDS buffers (rows of 576 B: conflict-free transposed reads) with the next chunk's
-// global loads in flight during the current chunk's MFMAs.  Partials [grid][O][I] are summed
-// in block order by k_splitk_reduce.
-constexpr int kFO = 256, kFI = 288, kFK = 64, kFPitch = 288;
+// k_wgrad_full: C[O][I] = sum_m Y[m][o] X[m][i] for O, I <= 256 (the learner's dW2 = dH2^T H1;
+// the bias column is summed by the fused kernel).  Every workgroup owns a contiguous range of
+// samples and the WHOLE output (8 waves x 32 output rows x 8 column tiles = 128 accumulator
+// registers per lane), so each activation row is read from HBM exactly once -- the tiled
+// k_wgrad_bf16 re-reads Y once per column tile and X once per row tile.  64-sample chunks are
+// staged through two LDS buffers (576-B rows: conflict-free transposed reads); two chunks'
+// global loads are in flight in registers while the current chunk's MFMAs run (one chunk per
+// CU in flight left HBM at 3.6 TB/s).  Partials [grid][O][I] are summed in a fixed order.
+constexpr int kFO = 256, kFI = 256, kFK = 64, kFPitch = 288;
+constexpr int kFPieces = kFK * (kFO / 8 + kFI / 8), kFPer = (kFPieces + 511) / 512;
+
+// Chunk loads through buffer descriptors based at the workgroup's first row: rows past the end
+// of the array come back as zeros from the hardware range check, so every load is issued
+// unconditionally (no per-piece branch) and the wait for a chunk is a counted vmcnt that leaves
+// the next chunk in flight.  Columns past O / I only feed accumulator rows / columns that are
+// never stored.
+template <int kU>
+__device__ __forceinline__ void wfull_fetch(__amdgpu_buffer_rsrc_t ry, __amdgpu_buffer_rsrc_t rx, int64_t ldy,
+                                            int64_t ldx, int64_t r0, int tid, bf16x8 (&v)[kU]) {
+    asm volatile("" : "+v"(tid));  // recompute the piece offsets per chunk (not hoisted into registers)
+    static_assert(kFK * (kFO / 8) == 4 * 512, "pieces 0..3 of a thread are Y, 4..7 are X");
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const bool isy = u < 4;  // compile-time per piece: one uniform descriptor per load
+        const int cc = tid + 512 * (isy ? u : u - 4);
+        const int row = cc >> 5, col = 8 * (cc & 31);
+        const int64_t m = r0 + row;  // row relative to the workgroup's first row
+        const auto t = isy ? __builtin_amdgcn_raw_buffer_load_b128(ry, (int)((m * ldy + col) * 2), 0, 0)
+                           : __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((m * ldx + col) * 2), 0, 0);
+        v[u] = __builtin_bit_cast(bf16x8, t);
+    }
+}
+
+template <int kU>
+__device__ __forceinline__ void wfull_stash(bf16* Ysb, bf16* Xsb, int tid, const bf16x8 (&v)[kU]) {
+    asm volatile("" : "+v"(tid));
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const int c = tid + 512 * u;
+        const bool isy = c < kFK * (kFO / 8);
+        const int cc = isy ? c : c - kFK * (kFO / 8);
+        const int row = cc >> 5, col = 8 * (cc & 31);
+        *reinterpret_cast<bf16x8*>((isy ? Ysb : Xsb) + row * kFPitch + col) = v[u];
+    }
+}
 
 __global__ __launch_bounds__(512, 1) void k_wgrad_full(WgradArgs w) {
     extern __shared__ __attribute__((aligned(16))) bf16 fsm[];
-    const auto Ys = [&](int b) { return fsm + b * kFK * kFPitch; };
-    const auto Xs = [&](int b) { return fsm + (2 + b) * kFK * kFPitch; };
+    bf16* const Y0 = fsm;
+    bf16* const Y1 = fsm + kFK * kFPitch;
+    bf16* const X0 = fsm + 2 * kFK * kFPitch;
+    bf16* const X1 = fsm + 3 * kFK * kFPitch;
+    const bf16* const Y = w.Y;
+    const bf16* const X = w.X;
+    const int64_t ldy = w.ldy, ldx = w.ldx;
+    const int O = w.O, I = w.I;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t mb = (int64_t)blockIdx.x * w.m_chunk;
     const int64_t me = min(w.M, mb + w.m_chunk);
-    const bool wave_live = 32 * wave < w.O;
-    f32x16 acc[9];
+    const bool wave_live = 32 * wave < O;
+    f32x16 acc[8];
 #pragma unroll
-    for (int j = 0; j < 9; ++j)
+    for (int j = 0; j < 8; ++j)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[j][q] = 0.0f;
-    // chunk = 64 rows x (32 Y + 36 X) 16-byte pieces = 4352 pieces, <= 9 per thread
-    constexpr int kPieces = kFK * (kFO / 8 + kFI / 8), kPer = (kPieces + 511) / 512;
-    bf16x8 pre[kPer];
-    auto fetch = [&](int64_t m0) {
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) {
-            const int c = tid + 512 * u;
-            bf16x8 v = zero8();
-            if (c < kPieces) {
-                const bool isy = c < kFK * (kFO / 8);
-                const int cc = isy ? c : c - kFK * (kFO / 8);
-                const int per = isy ? kFO / 8 : kFI / 8;
-                const int row = cc / per, col = 8 * (cc % per);
-                const int64_t m = m0 + row;
-                if (m < me && col < (isy ? w.O : w.I))
-                    v = *reinterpret_cast<const bf16x8*>(isy ? w.Y + m * w.ldy + col : w.X + m * w.ldx + col);
-            }
-            pre[u] = v;
-        }
-    };
-    auto stash = [&](int b) {
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) {
-            const int c = tid + 512 * u;
-            if (c < kPieces) {
-                const bool isy = c < kFK * (kFO / 8);
-                const int cc = isy ? c : c - kFK * (kFO / 8);
-                const int per = isy ? kFO / 8 : kFI / 8;
-                const int row = cc / per, col = 8 * (cc % per);
-                *reinterpret_cast<bf16x8*>((isy ? Ys(b) : Xs(b)) + row * kFPitch + col) = pre[u];
-            }
-        }
-    };
-    int b = 0;
-    if (mb < me) {
-        fetch(mb);
-        stash(0);
-    }
-    __syncthreads();
-    for (int64_t m0 = mb; m0 < me; m0 += kFK) {
-        const bool more = m0 + kFK < me;
-        if (more) fetch(m0 + kFK);
+    const auto compute = [&](const bf16* Ysb, const bf16* Xsb) {
 #pragma unroll
         for (int kk = 0; kk < kFK; kk += 16) {
-            const bf16x8 a = tr_frag<kFPitch>(Ys(b), 32 * wave, kk, lane);
+            // issue every fragment of this k-step before its MFMAs (one LDS latency per k-step,
+            // not one per MFMA)
+            const bf16x8 a = tr_frag<kFPitch>(Ysb, 32 * wave, kk, lane);
+            bf16x8 bb[8];
 #pragma unroll
-            for (int j = 0; j < 9; ++j) {
-                const bf16x8 bb = tr_frag<kFPitch>(Xs(b), 32 * j, kk, lane);
-                if (wave_live) acc[j] = mfma32(a, bb, acc[j]);
-            }
+            for (int j = 0; j < 8; ++j) bb[j] = tr_frag<kFPitch>(Xsb, 32 * j, kk, lane);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (wave_live) acc[j] = mfma32(a, bb[j], acc[j]);
+            __builtin_amdgcn_sched_barrier(0);
         }
-        if (more) stash(b ^ 1);
-        __syncthreads();
-        b ^= 1;
+    };
+    // LDS-only barrier: the register-staged loads of the chunks in flight must survive it
+    // (__syncthreads' fence would drain them with vmcnt(0))
+    const auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    // descriptors from wave-uniform values: based at row mb, bounded by the array end (M rows)
+    const int64_t yb = min((int64_t)0x7fffffff, (w.M - mb) * ldy * 2), xb = min((int64_t)0x7fffffff, (w.M - mb) * ldx * 2);
+    const auto uniform_ptr = [](const void* q) {
+        const uint64_t a = reinterpret_cast<uint64_t>(q);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+        return reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    };
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(Y + mb * ldy), 0,
+                                                                        __builtin_amdgcn_readfirstlane((int)yb), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(X + mb * ldx), 0,
+                                                                        __builtin_amdgcn_readfirstlane((int)xb), 0x00020000);
+    bf16x8 f0[kFPer], f1[kFPer];
+    wfull_fetch(ry, rx, ldy, ldx, 0, tid, f0);
+    wfull_stash(Y0, X0, tid, f0);
+    wfull_fetch(ry, rx, ldy, ldx, kFK, tid, f0);  // chunk 1 in flight
+    __syncthreads();
+    // chunk c sits in LDS buffer c & 1, chunk c + 1 in registers; chunk c + 2 is issued first.
+    // Chunks past the workgroup's range are fetched but never computed; rows past M read as 0.
+    for (int64_t m0 = mb; m0 < me; m0 += 2 * kFK) {
+        wfull_fetch(ry, rx, ldy, ldx, m0 - mb + 2 * kFK, tid, f1);
+        compute(Y0, X0);
+        lds_barrier();  // every wave is done reading buffer 1 (chunk c - 1)
+        wfull_stash(Y1, X1, tid, f0);
+        lds_barrier();
+        if (m0 + kFK >= me) break;
+        wfull_fetch(ry, rx, ldy, ldx, m0 - mb + 3 * kFK, tid, f0);
+        compute(Y1, X1);
+        lds_barrier();
+        wfull_stash(Y0, X0, tid, f1);
+        lds_barrier();
     }
     if (!wave_live) return;
-    float* dst = w.partial ? w.partial + (int64_t)blockIdx.x * w.O * w.I : w.out;
+    float* dst = w.partial ? w.partial + (int64_t)blockIdx.x * O * I : w.out;
+    const int64_t ld = w.partial ? I : w.ldo;
 #pragma unroll
-    for (int j = 0; j < 9; ++j) {
+    for (int j = 0; j < 8; ++j) {
         const int i = 32 * j + (lane & 31);
-        if (i >= w.I) continue;
+        if (i >= I) continue;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int o = 32 * wave + acc_row(q, lane);
-            if (o < w.O) dst[(int64_t)o * w.I + i] = acc[j][q];
+            if (o < O) dst[(int64_t)o * ld + i] = acc[j][q];
         }
+    }
+}
+
+// ------------------------------------------------------------------ dW2 via LDS-DMA
+// k_wgrad_glds: the same whole-output contraction for O = I = 256 with the sample chunks
+// streamed HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging): a 4-buffer ring of
+// 32-sample chunks keeps three chunks (96 KB per CU) in flight across raw s_barriers with
+// counted vmcnt waits.  LDS rows are 512 B unpadded; the 16-byte chunks of row r are XOR-
+// swizzled by 4 (r & 3) on the SOURCE address (the LDS-DMA destination is lane-linear), which
+// keeps the transposed fragment reads conflict-free.
+constexpr int kGK = 32, kGNB = 4, kGRowB = 512;
+constexpr int kGChunkB = 2 * kGK * kGRowB;  // Y + X bytes of one chunk
+
+__device__ __forceinline__ bf16x8 tr_frag_swz(const bf16* tile, int col0, int kk, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int col = col0 + 16 * (g & 1) + 4 * p;
+    lds_bf16* base = (lds_bf16*)(tile);
+    const auto at = [&](int row) {
+        return (lds_bf16x4*)(base + row * (kGRowB / 2) + (((col >> 3) ^ (4 * (row & 3))) << 3) + (col & 7));
+    };
+    const int row = kk + 8 * (g >> 1) + q;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(at(row));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(at(row + 4));
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = lo[j];
+        v[4 + j] = hi[j];
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(512, 1) void k_wgrad_glds(WgradArgs w) {
+    extern __shared__ __attribute__((aligned(16))) char gsm[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // chunks blockIdx.x, blockIdx.x + grid, ...: at any moment the workgroups stream neighbouring
+    // 32-row chunks, spread over all HBM channels (contiguous per-workgroup ranges 1.6 MB apart
+    // made every CU hit the same channels in lockstep)
+    const int64_t total = w.M / kGK;
+    const int nch = (int)((total - blockIdx.x + gridDim.x - 1) / gridDim.x);
+    const bf16* const Y = w.Y;
+    const bf16* const X = w.X;
+    const int64_t ldy = w.ldy, ldx = w.ldx;
+    f32x16 acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[j][q] = 0.0f;
+    // chunk c -> ring slot c % 4; wave w issues pieces 4w .. 4w + 3 (2 rows of Y or X each)
+    const auto issue = [&](int c) {
+        char* buf = gsm + (c % kGNB) * kGChunkB;
+        const int64_t m0 = ((int64_t)blockIdx.x + (int64_t)c * gridDim.x) * kGK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int pc = 4 * wave + i;
+            const bool isy = pc < 16;
+            const int prow = 2 * (pc & 15);
+            const int r = prow + (lane >> 5), slot = lane & 31;
+            const int gchunk = slot ^ (4 * (r & 3));
+            const bf16* src = isy ? Y + (m0 + r) * ldy + 8 * gchunk : X + (m0 + r) * ldx + 8 * gchunk;
+            char* dst = buf + (isy ? 0 : kGK * kGRowB) + prow * kGRowB;
+            // issued from inline asm so the compiler's waitcnt pass does not see an LDS write in
+            // flight (it would put vmcnt(0) before every LDS read); the counted waits below own it
+            const uint32_t lds_addr = __builtin_amdgcn_readfirstlane(
+                (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)dst);
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(src), "s"(lds_addr)
+                : "memory");
+        }
+    };
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+        if (c < nch) issue(c);
+    for (int c = 0; c < nch; ++c) {
+        // chunk c has landed once at most the chunks issued after it are outstanding
+        const int after = min(2, nch - 1 - c);
+        if (after == 2) __builtin_amdgcn_s_waitcnt(0xF78);       // vmcnt(8)
+        else if (after == 1) __builtin_amdgcn_s_waitcnt(0xF74);  // vmcnt(4)
+        else __builtin_amdgcn_s_waitcnt(0xF70);                  // vmcnt(0)
+        __builtin_amdgcn_s_barrier();  // every wave's DMA for chunk c is in; compute(c - 1) is done
+        if (c + 3 < nch) issue(c + 3);  // into the slot compute(c - 1) just released
+        const bf16* Ys = (const bf16*)(gsm + (c % kGNB) * kGChunkB);
+        const bf16* Xs = (const bf16*)(gsm + (c % kGNB) * kGChunkB + kGK * kGRowB);
+        if (w.diag & 1) continue;
+        // both k-steps' fragments are issued before the first MFMA (one LDS latency per chunk)
+        bf16x8 a[2], bb[2][8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            a[h] = tr_frag_swz(Ys, 32 * wave, 16 * h, lane);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bb[h][j] = tr_frag_swz(Xs, 32 * j, 16 * h, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] = mfma32(a[h], bb[h][j], acc[j]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    float* dst = w.partial ? w.partial + (int64_t)blockIdx.x * w.O * w.I : w.out;
+    const int64_t ld = w.partial ? w.I : w.ldo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int i = 32 * j + (lane & 31);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dst[(int64_t)(32 * wave + acc_row(q, lane)) * ld + i] = acc[j][q];
     }
 }
 
 // out[i] (+)= sum_z partial[z][i], fixed order (deterministic)
 __global__ void k_splitk_reduce(const float* __restrict__ partial, int64_t slab, int z, float* __restrict__ out,
-                                int accumulate) {
+                                int accumulate, int cols, int64_t ldo) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= slab) return;
     float s = 0.0f;
     for (int k = 0; k < z; ++k) s += partial[(int64_t)k * slab + i];
-    out[i] = accumulate ? out[i] + s : s;
+    const int64_t o = cols ? (i / cols) * ldo + i % cols : i;  // [rows][cols] slab -> [rows][ldo] output
+    out[o] = accumulate ? out[o] + s : s;
 }
 
 // First level of a two-level slab sum: tmp[g][i] = sum of slabs g*z/G .. (g+1)*z/G - 1 (in order),
@@ -441,7 +594,7 @@ __global__ void k_slab_group_sum(const float* __restrict__ partial, int64_t slab
 }
 
 int launch_slab_reduce(const float* partial, int64_t slab, int z, float* tmp, float* out, int accumulate,
-                       hipStream_t st) {
+                       hipStream_t st, int cols, int64_t ldo) {
     const unsigned nb = (unsigned)((slab + 255) / 256);
     if (z > kReduceGroups && tmp) {
         hipLaunchKernelGGL(k_slab_group_sum, dim3(nb, kReduceGroups), dim3(256), 0, st, partial, slab, z, tmp);
@@ -449,7 +602,7 @@ int launch_slab_reduce(const float* partial, int64_t slab, int z, float* tmp, fl
         partial = tmp;
         z = kReduceGroups;
     }
-    hipLaunchKernelGGL(k_splitk_reduce, dim3(nb), dim3(256), 0, st, partial, slab, z, out, accumulate);
+    hipLaunchKernelGGL(k_splitk_reduce, dim3(nb), dim3(256), 0, st, partial, slab, z, out, accumulate, cols, ldo);
     return launch_check("k_splitk_reduce");
 }
 
@@ -484,7 +637,8 @@ int launch_gemm(const GemmArgs& g0, int splits, float* reduce_out, int accumulat
 }
 
 int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, int I, int64_t M, int splits,
-                 float* partial, float* out, hipStream_t st) {
+                 float* partial, float* out, hipStream_t st, int64_t ldo) {
+    if (ldo <= 0) ldo = I;
     DXRL_REQUIRE(Y && X && out && O > 0 && I > 0 && M > 0, "wgrad: bad arguments");
     DXRL_REQUIRE(ldy % 8 == 0 && ldx % 8 == 0 && O % 8 == 0 && I % 8 == 0,
                  "wgrad: leading dims and feature counts must be multiples of 8");
@@ -495,8 +649,29 @@ int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, 
     chunk = (chunk + kWK - 1) / kWK * kWK;
     splits = (int)((M + chunk - 1) / chunk);
     DXRL_REQUIRE(splits == 1 || partial, "wgrad: split-K needs a partial slab");
-    WgradArgs w{Y, ldy, X, ldx, O, I, M, chunk, out, splits > 1 ? partial : nullptr};
-    if (O <= kFO && I <= kFI && O > 128 && M >= (int64_t)splits * kFK) {  // whole output per workgroup
+    WgradArgs w{Y, ldy, X, ldx, O, I, M, chunk, out, splits > 1 ? partial : nullptr, ldo, 0};
+    if (O == kFO && I == kFI && M % kGK == 0 && ldy >= kFO && ldx >= kFI &&
+        getenv("DXRL_WGRAD_REGSTAGE") == nullptr) {  // LDS-DMA stream (A/B: DXRL_WGRAD_REGSTAGE=1)
+        static bool attr = [] {
+            return hipFuncSetAttribute(reinterpret_cast<const void*>(k_wgrad_glds),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kGNB * kGChunkB) == hipSuccess;
+        }();
+        DXRL_REQUIRE(attr, "wgrad: could not raise the dynamic LDS limit");
+        static const int diag = [] {
+            const char* v = getenv("DXRL_WGRAD_DIAG");
+            return v ? atoi(v) : 0;
+        }();
+        w.diag = diag;
+        hipLaunchKernelGGL(k_wgrad_glds, dim3((unsigned)splits), dim3(512), kGNB * kGChunkB, st, w);
+        if (int rc = launch_check("k_wgrad_glds")) return rc;
+        if (splits > 1) {
+            const int64_t slab = (int64_t)O * I;
+            return launch_slab_reduce(partial, slab, splits, partial + (int64_t)splits * slab, out, 0, st, I, ldo);
+        }
+        return DXRL_OK;
+    }
+    if (O <= kFO && I <= kFI && O > 128 && M >= (int64_t)splits * kFK && chunk % kFK == 0 &&
+        (M + 3 * kFK) * (ldy > ldx ? ldy : ldx) * 2 < 0x7fffffff) {  // whole output per workgroup
         static bool attr = [] {
             return hipFuncSetAttribute(reinterpret_cast<const void*>(k_wgrad_full),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kFK * kFPitch * 2) == hipSuccess;
@@ -506,7 +681,7 @@ int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, 
         if (int rc = launch_check("k_wgrad_full")) return rc;
         if (splits > 1) {
             const int64_t slab = (int64_t)O * I;
-            return launch_slab_reduce(partial, slab, splits, partial + (int64_t)splits * slab, out, 0, st);
+            return launch_slab_reduce(partial, slab, splits, partial + (int64_t)splits * slab, out, 0, st, I, ldo);
         }
         return DXRL_OK;
     }
@@ -515,7 +690,8 @@ int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, 
     if (int rc = launch_check("k_wgrad_bf16")) return rc;
     if (splits > 1) {
         const int64_t slab = (int64_t)O * I;
-        if (int rc = launch_slab_reduce(partial, slab, splits, partial + (int64_t)splits * slab, out, 0, st)) return rc;
+        if (int rc = launch_slab_reduce(partial, slab, splits, partial + (int64_t)splits * slab, out, 0, st, I, ldo))
+            return rc;
     }
     return DXRL_OK;
 }

@@ -381,7 +381,7 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout(PgRolloutA
 // closure term, log pi) are gathered through a per-env LDS row and added in the reference order
 // on every lane.  The actor MLP runs on all four waves as in k_pg_rollout, on one 32-row
 // MFMA tile of which rows 0..15 are this workgroup's envs.
-constexpr int kLsEnvs = 16, kLsLanes = 16;
+constexpr int kLsEnvs = 16;  // 16 lanes per env: envs per workgroup = 256 threads / 16
 
 // standard normal k of Philox block k / 4 (Box-Muller pairs (x, y), (z, w)), as philox_normals
 __device__ __forceinline__ float philox_normal_at(int k, uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream) {

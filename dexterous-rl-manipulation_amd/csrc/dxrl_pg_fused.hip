@@ -12,7 +12,7 @@
 //             dW1 += dH1^T X              (registers, whole launch)
 //
 // H1 and dH2 go to HBM once so the one contraction too large to keep in
-// registers, dW2 = dH2^T [H1 | 1], runs as the split-K weight-gradient GEMM
+// registers, dW2 = dH2^T H1, runs as the whole-output weight-gradient GEMM
 // (launch_wgrad) right after.  Nothing else of the activations ever leaves
 // the CU: compared with the layer-by-layer GEMM chain this removes the H2,
 // dH1, mu / dout round trips and five of the eight launches.
@@ -56,7 +56,8 @@ constexpr int kHW = kTR / 32;            // waves running the heads (one 32-samp
 constexpr int kPartW1 = 0;                   // [256][64]
 constexpr int kPartW3 = kPartW1 + kH * kIn;  // [32][288]
 constexpr int kPartLs = kPartW3 + kOut * kHx;
-constexpr int kPartSize = kPartLs + 16;
+constexpr int kPartB2 = kPartLs + 16;        // [2][256]: dL/db2 column sums, two row halves
+constexpr int kPartSize = kPartB2 + 2 * kH;
 
 // global-address-space views: loads through them compile to global_load (vmcnt only); a
 // generic pointer the compiler cannot place compiles to flat_load, which also counts in
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
     bf16* H2 = lds + kOffH2;
     bf16* D = lds + kOffD;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r = lane & 31, h = lane >> 5;
+    const int r = lane & 31;
     const int ft0 = kNT * wave;  // this wave's first 32-wide feature tile
     const int64_t ntiles = (p.rows + kTR - 1) / kTR;
 
@@ -223,6 +224,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
     float dls[8], db3[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) dls[j] = db3[j] = 0.0f;
+    float db2 = 0.0f;  // dL/db2 of column tid % 256 over this thread's row half of every tile
     double lsum[4] = {0.0, 0.0, 0.0, 0.0};
 
     const double adv_mean = kTrain && p.net == 0 ? p.stats[2] : 0.0;
@@ -442,13 +444,22 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
         __syncthreads();
         STAMP(10);
 
-        // ---- dH2 -> HBM; dH1 = (dH2 W2) * (1 - H1^2)  (wave w: L2 inputs of its tiles, rows = samples)
+        // ---- dH2 -> HBM (Y of the dW2 GEMM), db2 += column sums of dH2,
+        //      dH1 = (dH2 W2) * (1 - H1^2)  (wave w: L2 inputs of its tiles, rows = samples)
 #pragma unroll 4
         for (int c = tid; c < kTR * (kH / 8); c += kFThreads) {
             const int row = c >> 5, col = 8 * (c & 31);
             const int64_t m = m0 + row;
             if (m < p.rows && !(p.diag & 1))
                 *reinterpret_cast<bf16x8*>(p.dh2_out + m * kH + col) = *reinterpret_cast<const bf16x8*>(H2 + row * kHp + col);
+        }
+        {
+            constexpr int kRowsPer = kTR * kH / kFThreads;  // rows of one column per thread per tile
+            const int col = tid & (kH - 1), r0 = (tid / kH) * kRowsPer;
+            float sc = 0.0f;  // padding rows carry dH2 = 0 (their dout is 0)
+#pragma unroll 8
+            for (int rr = 0; rr < kRowsPer; ++rr) sc += from_bf16(H2[(r0 + rr) * kHp + col]);
+            db2 += sc;
         }
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
@@ -497,6 +508,9 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
 #pragma unroll
             for (int it = 0; it < 2; ++it) part[kPartW1 + (32 * (ft0 + j) + o) * kIn + 32 * it + r] = acc1[j][it][q];
         }
+    // db2 halves (4 waves: one 128-row half per thread, the other half slot is zero)
+    part[kPartB2 + tid] = db2;
+    if (kFThreads == kH) part[kPartB2 + kH + tid] = 0.0f;
     float* red = reinterpret_cast<float*>(lds);              // [head lanes][16]
     double* lred = reinterpret_cast<double*>(lds + kOffH1);  // [head lanes][4]
     if (wave < kHW) {
@@ -532,9 +546,17 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
 
 // grads blocks W1 / W3 (and log_std for the actor) from the workgroup sum (launch_slab_reduce)
 __global__ void k_fused_scatter(const float* __restrict__ sum, float* __restrict__ gW1, float* __restrict__ gW3,
-                                float* __restrict__ gLs, float ent_coef) {
+                                float* __restrict__ gLs, float* __restrict__ gW2, float ent_coef) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= kPartSize) return;
+    if (j >= kPartB2) {  // W2 block column 256 (bias) and the zero pad columns 257..287 of row n
+        const int n = j - kPartB2;
+        if (n < kH) {
+            gW2[(int64_t)n * kHx + kH] = sum[kPartB2 + n] + sum[kPartB2 + kH + n];
+            for (int c = kH + 1; c < kHx; ++c) gW2[(int64_t)n * kHx + c] = 0.0f;
+        }
+        return;
+    }
     const int col = (j - kPartW3) % kHx;
     const bool w3pad = j >= kPartW3 && j < kPartLs && col > kH;  // never written by k_pg_fused
     const float s = w3pad ? 0.0f : sum[j];
@@ -642,11 +664,11 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     float* sum = tmp + (int64_t)kReduceGroups * kPartSize;
     if (int rc = launch_slab_reduce(a->partial, kPartSize, grid, tmp, sum, 0, st)) return rc;
     hipLaunchKernelGGL(k_fused_scatter, dim3((kPartSize + 255) / 256), dim3(256), 0, st, sum,
-                       G + (c ? kOffW1c : kOffW1a), G + o3, c ? nullptr : G + kOffLogStd, (float)a->ent_coef);
+                       G + (c ? kOffW1c : kOffW1a), G + o3, c ? nullptr : G + kOffLogStd, G + o2, (float)a->ent_coef);
     if (int rc = launch_check("k_fused_scatter")) return rc;
-    // dW2 = dH2^T [H1 | 1]: bias gradient lands in column 256
-    return launch_wgrad(static_cast<const bf16*>(a->dh2), kH, kH, static_cast<const bf16*>(a->h1), kHx, kHx, a->rows,
-                        a->wgrad_splits, a->wgrad_partial, G + o2, st);
+    // dW2[:, 0..255] = dH2^T H1 (the bias column 256 came from the column sums above)
+    return launch_wgrad(static_cast<const bf16*>(a->dh2), kH, kH, static_cast<const bf16*>(a->h1), kHx, kH, a->rows,
+                        a->wgrad_splits, a->wgrad_partial, G + o2, st, kHx);
 }
 
 }  // extern "C"

@@ -136,7 +136,7 @@ class PGTrainer:
         self.dls_partial = z((M + 255) // 256, ACT_PAD)
         self.loss_partial = torch.zeros((M + 255) // 256, 4, dtype=torch.float64, device=d)
         self.dH2, self.dH1 = z(M, H, dt=bf), z(M, H, dt=bf)
-        self.splits = max(1, min(cfg.splitk_target_blocks // 3, M // 4096))  # dW2: one workgroup per CU
+        self.splits = max(1, min(cfg.splitk_target_blocks // 3, M // 1024))  # dW2: one workgroup per CU
         self.kpartial = z(self.splits + 16, H, HX)  # + two-level reduction scratch
         self.gnorm2 = torch.zeros(1, dtype=torch.float64, device=d)
         tr_, pf_ = C.c_int32(), C.c_int64()

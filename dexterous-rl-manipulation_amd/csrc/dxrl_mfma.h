@@ -30,6 +30,13 @@ __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// v_mfma_f32_16x16x32_bf16: lane l holds A[l & 15][8 (l >> 4) ..+7], Bt[l & 15][8 (l >> 4) ..+7];
+// accumulator: col = l & 15, row = 4 (l >> 4) + reg
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 __device__ __forceinline__ bf16 to_bf16(float x) { return (bf16)x; }  // v_cvt_pk_bf16_f32 (RNE)
 __device__ __forceinline__ float from_bf16(bf16 x) { return (float)x; }
 
@@ -53,6 +60,25 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int col0, int kk, in
     const int row = kk + 8 * (g >> 1) + q;
     const int col = col0 + 16 * (g & 1) + 4 * p;
     lds_bf16* base = (lds_bf16*)(tile);  // generic -> LDS address space (the tile is __shared__)
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + row * kPitch + col));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + (row + 4) * kPitch + col));
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = lo[j];
+        v[4 + j] = hi[j];
+    }
+    return v;
+}
+
+// The same for the 16x16x32 operand: lane l gets T[kk + 8 (l >> 4) + j][col0 + (l & 15)], j = 0..7
+// (operand row "feature col0 + (l & 15)" over the 32 k values kk..kk+31).
+template <int kPitch>
+__device__ __forceinline__ bf16x8 tr_frag16(const bf16* tile, int col0, int kk, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int row = kk + 8 * g + q;
+    const int col = col0 + 4 * p;
+    lds_bf16* base = (lds_bf16*)(tile);
     const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + row * kPitch + col));
     const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + (row + 4) * kPitch + col));
     bf16x8 v;

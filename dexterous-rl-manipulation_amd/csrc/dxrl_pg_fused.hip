@@ -56,8 +56,8 @@ constexpr int kHW = kTR / 32;            // waves running the heads (one 32-samp
 constexpr int kPartW1 = 0;                   // [256][64]
 constexpr int kPartW3 = kPartW1 + kH * kIn;  // [32][288]
 constexpr int kPartLs = kPartW3 + kOut * kHx;
-constexpr int kPartB2 = kPartLs + 16;        // [2][256]: dL/db2 column sums, two row halves
-constexpr int kPartSize = kPartB2 + 2 * kH;
+constexpr int kPartB2 = kPartLs + 16;        // [256]: dL/db2 column sums
+constexpr int kPartSize = kPartB2 + kH;
 
 // global-address-space views: loads through them compile to global_load (vmcnt only); a
 // generic pointer the compiler cannot place compiles to flat_load, which also counts in
@@ -97,9 +97,12 @@ __device__ __forceinline__ void zero_acc(f32x16& a) {
 // acc[j][mt] (features 32 (ft0 + j).. x samples 32 mt..) = W[32 (ft0 + j) + r][:] . A[32 mt + r][:]
 // over KS k-steps.  Weight fragments stream from L2 one 4-k-step chunk ahead (double
 // buffer); each activation fragment read from LDS feeds NT MFMAs.
-template <int KS, int kLda, int NT>
+struct NoHook {
+    __device__ void operator()() const {}
+};
+template <int KS, int kLda, int NT, typename Hook = NoHook>
 __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int ldw, int ft0, const bf16* A,
-                                          f32x16 (&acc)[NT][4], int lane) {
+                                          f32x16 (&acc)[NT][4], int lane, Hook hook = Hook{}) {
     static_assert(NT == 1, "one feature tile per call");
     const int r = lane & 31, h = lane >> 5;
     constexpr int kD = KS < 8 ? KS : 8;  // weight prefetch distance (k-steps)
@@ -125,6 +128,9 @@ __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int ldw, i
         }
         const bf16x8 a = wf[k % kD];
         if (k + kD < KS) wf[k % kD] = wp[2 * (k + kD)];
+        // loads the caller wants behind the last weight fragment (vmcnt retires in issue order:
+        // issued earlier they would hold every weight wait of this call)
+        if (k + kD == KS) hook();
         // keep the prefetches above issued ahead of this k-step's MFMAs (the scheduler would
         // otherwise sink every load next to its use and expose its full latency)
         __builtin_amdgcn_sched_barrier(0);
@@ -135,17 +141,17 @@ __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int ldw, i
 }
 
 // tanh(acc + bias) -> bf16 row-major activation tile (4 consecutive features per 8-byte store)
-__device__ __forceinline__ void store_hidden(const f32x16 (&acc)[1][4], int ft, const float* __restrict__ bias,
-                                             bf16* H, int lane) {
+// (bk: the lane's 16 pre-scaled biases tanh_bias(b[32 ft + 8 g + 4 h + u]) at [4 g + u], or null)
+__device__ __forceinline__ void store_hidden(const f32x16 (&acc)[1][4], int ft, const float* bk, bf16* H, int lane) {
     const int r = lane & 31, h = lane >> 5;
     constexpr int j = 0;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int f0 = 32 * ft + 8 * g + 4 * h;
             float b[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (bias) {
+            if (bk) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) b[u] = tanh_bias(((gf32*)bias)[(int64_t)(f0 + u) * kHx]);
+                for (int u = 0; u < 4; ++u) b[u] = bk[4 * g + u];
             }
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
@@ -186,6 +192,24 @@ __device__ __forceinline__ void gate_in_place(const f32x16 (&acc)[1][4], int ft,
         }
 }
 
+// A [kTR][kH] bf16 tile of LDS (pitch kHp) -> rows m0.. of an HBM matrix (leading dimension ld),
+// nthr threads from thread index t0 (16-byte chunks, rows past `rows` skipped)
+template <int kThreads>
+__device__ __forceinline__ void copy_tile_out_n(const bf16* T, bf16* out, int64_t ld, int64_t m0, int64_t rows,
+                                                int t, int diag) {
+    constexpr int kChunks = kTR * (kH / 8);
+    static_assert(kChunks % kThreads == 0, "whole chunks per thread");
+    if (diag & 1) return;
+    asm volatile("" : "+v"(t));  // per-call addresses (hoisted out of the tile loop they would spill)
+#pragma unroll
+    for (int u = 0; u < kChunks / kThreads; ++u) {
+        const int c = t + kThreads * u, row = c >> 5, col = 8 * (c & 31);
+        const int64_t m = m0 + row;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(T + row * kHp + col);
+        if (m < rows) *(__attribute__((address_space(1))) bf16x8*)(out + m * ld + col) = v;
+    }
+}
+
 // Hide a pointer's provenance from the optimiser so loads through it are not hoisted
 // out of the tile loop (loop-invariant weight / bias loads would otherwise pin registers
 // for the whole launch).
@@ -209,23 +233,28 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
     bf16* H2 = lds + kOffH2;
     bf16* D = lds + kOffD;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r = lane & 31;
     const int ft0 = kNT * wave;  // this wave's first 32-wide feature tile
     const int64_t ntiles = (p.rows + kTR - 1) / kTR;
 
     // launch-long accumulators: dW3 columns of this wave's tiles, dW1 rows of this wave's tiles
-    f32x16 acc3[kNT], acc1[kNT][2];
+    // (16x16x32 tiles: only head rows 0..15 and input columns 0..47 can be nonzero -- 15 mu rows /
+    // one value row, 45 observation features + the bias column -- so 8 + 24 registers, not 16 + 32)
+    f32x4 acc3[kNT][2], acc1[kNT][2][3];
 #pragma unroll
-    for (int j = 0; j < kNT; ++j) {
-        zero_acc(acc3[j]);
-        zero_acc(acc1[j][0]);
-        zero_acc(acc1[j][1]);
-    }
+    for (int j = 0; j < kNT; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            acc3[j][0][q] = acc3[j][1][q] = 0.0f;
+#pragma unroll
+            for (int ri = 0; ri < 2; ++ri)
+#pragma unroll
+                for (int ci = 0; ci < 3; ++ci) acc1[j][ri][ci][q] = 0.0f;
+        }
     float dls[8], db3[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) dls[j] = db3[j] = 0.0f;
-    float db2 = 0.0f;  // dL/db2 of column tid % 256 over this thread's row half of every tile
-    double lsum[4] = {0.0, 0.0, 0.0, 0.0};
+    float db2 = 0.0f;  // threads < 256: dL/db2 of column tid
+    float lsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // per-thread sums over <= ~25 tiles (f64 across threads)
 
     const double adv_mean = kTrain && p.net == 0 ? p.stats[2] : 0.0;
     const double adv_div = kTrain && p.net == 0 ? p.stats[4] + 1e-8 : 1.0;
@@ -234,9 +263,11 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
     constexpr int kXU = kTR * (kIn / 8) / kFThreads;
     bf16x8 xr[kXU];
     auto fetch_x = [&](int64_t tile) {
+        int t = tid;
+        asm volatile("" : "+v"(t));
 #pragma unroll
         for (int u = 0; u < kXU; ++u) {
-            const int c = tid + kFThreads * u, row = c >> 3, col = 8 * (c & 7);
+            const int c = t + kFThreads * u, row = c >> 3, col = 8 * (c & 7);
             const int64_t m = tile * kTR + row;
             xr[u] = m < p.rows ? *reinterpret_cast<const bf16x8*>(p.X + m * kIn + col) : zero8();
         }
@@ -291,30 +322,78 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
         STAMP(2);
         __syncthreads();
         STAMP(3);
+        // head inputs (HBM), issued halfway through L2 so their latency hides behind its second half
+        const int ml = 32 * wave + r;
+        const int64_t m = m0 + ml;
+        const bool valid = m < p.rows;
+        float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+        float lo = 0.0f, adv = 0.0f, ret = 0.0f;
+        float bk[16];
+        int bft = ft0;  // feature tile whose biases bk holds
+        auto head_inputs = [&]() {
+            // the bias loads first: store_hidden waits for them, and must not wait for the HBM loads
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                bk[q] = tanh_bias(((gf32*)b2)[(int64_t)(32 * bft + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
+            if (!kTrain || __builtin_amdgcn_readfirstlane(wave) >= kHW) return;
+            const int64_t mc = valid ? m : p.rows - 1;  // clamped: unconditional loads, no branch
+            if (p.net == 0) {
+                a0 = *reinterpret_cast<const float4*>(p.act + mc * kActPad + 4 * h);
+                a1 = *reinterpret_cast<const float4*>(p.act + mc * kActPad + 8 + 4 * h);
+                lo = p.logp_old[mc];
+                adv = p.adv[mc];
+            } else {
+                ret = p.ret[mc];
+            }
+        };
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[1][4];
-            fwd_tiles<kH / 16, kHp, 1>(W2, kHx, ft0 + j, H1, acc, lane);
-            store_hidden(acc, ft0 + j, b2, H2, lane);
+            bft = ft0 + j;
+            fwd_tiles<kH / 16, kHp, 1>(W2, kHx, ft0 + j, H1, acc, lane, [&]() {
+                if (j == kNT - 1) head_inputs();
+                else {
+#pragma unroll
+                    for (int q = 0; q < 16; ++q)
+                        bk[q] = tanh_bias(((gf32*)b2)[(int64_t)(32 * bft + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
+                }
+            });
+            store_hidden(acc, ft0 + j, bk, H2, lane);
         }
         STAMP(4);
         __syncthreads();
         STAMP(5);
 
         // ---- head: wave w < kHW owns samples 32w .. 32w + 31 (lane: sample r, head rows of half h)
+        // H1 tile -> HBM (B operand of the dW2 GEMM) by the waves that have no head tile; their
+        // stores then retire while the head runs instead of holding the head's load waits
+        if constexpr (kTrain && kFW > kHW) {
+            if (wave >= kHW) copy_tile_out_n<64 * (kFW - kHW)>(H1, p.h1_out, kHx, m0, p.rows, tid - 64 * kHW, p.diag);
+        }
         if (wave < kHW) {
             f32x16 acc;
             zero_acc(acc);
+            // W3 fragments in two batches of 8 (32 registers in flight)
             const gbf16x8* wrow = (const gbf16x8*)(W3 + (int64_t)r * kHx + 8 * h);
+            constexpr int kB = kH / 32;  // fragments per batch (two batches: 32 registers in flight)
+            bf16x8 w3f[kB];
 #pragma unroll
-            for (int k = 0; k < kH / 16; ++k) {
-                const bf16x8 a = wrow[2 * k];
+            for (int k = 0; k < kB; ++k) w3f[k] = wrow[2 * k];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < kB; ++k) {
                 const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * k + 8 * h);
-                acc = mfma32(a, b, acc);
+                acc = mfma32(w3f[k], b, acc);
             }
-            const int ml = 32 * wave + r;
-            const int64_t m = m0 + ml;
-            const bool valid = m < p.rows;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < kB; ++k) w3f[k] = wrow[2 * (k + kB)];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < kB; ++k) {
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * (k + kB) + 8 * h);
+                acc = mfma32(w3f[k], b, acc);
+            }
             float d[8], b3v[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
@@ -329,14 +408,6 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
                         const int o = (q & 3) + 8 * (q >> 2) + 4 * h;
                         lsv[q] = o < kAct ? ((gf32*)logstd)[o] : 0.0f;
                         iv2[q] = __expf(-2.0f * lsv[q]);
-                    }
-                    float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
-                    float lo = 0.0f, adv = 0.0f;
-                    if (valid) {
-                        a0 = *reinterpret_cast<const float4*>(p.act + m * kActPad + 4 * h);
-                        a1 = *reinterpret_cast<const float4*>(p.act + m * kActPad + 8 + 4 * h);
-                        lo = p.logp_old[m];
-                        adv = p.adv[m];
                     }
                     a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w;
                     a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
@@ -381,9 +452,9 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
                             }
                         }
                         if (h == 0) {
-                            lsum[0] += -(double)fminf(s1, s2);
-                            lsum[2] += fabsf(ratio - 1.0f) > p.clip_eps ? 1.0 : 0.0;
-                            lsum[3] += (double)(lo - lp);
+                            lsum[0] += -fminf(s1, s2);
+                            lsum[2] += fabsf(ratio - 1.0f) > p.clip_eps ? 1.0f : 0.0f;
+                            lsum[3] += lo - lp;
                         }
                     }
                 }
@@ -392,10 +463,10 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
                 if (!kTrain) {
                     if (valid && h == 0) p.v_out[m] = v;
                 } else if (valid && h == 0) {
-                    const float e = v - p.ret[m];
+                    const float e = v - ret;
                     d[0] = from_bf16(to_bf16(p.vf2 * e * p.sc));
                     db3[0] += d[0];
-                    lsum[1] += (double)e * (double)e;
+                    lsum[1] += e * e;
                 }
             }
             if (kTrain) {
@@ -415,51 +486,49 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
             STAMP(7);
             continue;
         }
-        // H1 tile -> HBM (B operand of the dW2 GEMM): 128 rows x 32 chunks of 16 B
-#pragma unroll 4
-        for (int c = tid; c < kTR * (kH / 8); c += kFThreads) {
-            const int row = c >> 5, col = 8 * (c & 31);
-            const int64_t m = m0 + row;
-            if (m < p.rows && !(p.diag & 1))
-                *reinterpret_cast<bf16x8*>(p.h1_out + m * kHx + col) = *reinterpret_cast<const bf16x8*>(H1 + row * kHp + col);
-        }
+        if constexpr (kFW == kHW) copy_tile_out_n<kFThreads>(H1, p.h1_out, kHx, m0, p.rows, tid, p.diag);
         STAMP(7);
         __syncthreads();
         STAMP(8);
 
         // ---- dW3 += dout^T H2 (wave w: H2 columns of its tiles), then dH2 in place of H2
 #pragma unroll
-        for (int kk = 0; kk < kTR; kk += 16) {
-            const bf16x8 a = tr_frag<kDp>(D, 0, kk, lane);
+        for (int kk = 0; kk < kTR; kk += 32) {
+            const bf16x8 a = tr_frag16<kDp>(D, 0, kk, lane);
 #pragma unroll
-            for (int j = 0; j < kNT; ++j) if (!(p.diag & 4)) acc3[j] = mfma32(a, tr_frag<kHp>(H2, 32 * (ft0 + j), kk, lane), acc3[j]);
+            for (int j = 0; j < kNT; ++j)
+#pragma unroll
+                for (int ci = 0; ci < 2; ++ci)
+                    if (!(p.diag & 4))
+                        acc3[j][ci] = mfma16(a, tr_frag16<kHp>(H2, 32 * (ft0 + j) + 16 * ci, kk, lane), acc3[j][ci]);
         }
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[1][4];
-            fwd_tiles<kOut / 16, kDp, 1>(W3T, kOut, ft0 + j, D, acc, lane);  // dH2^T = W3^T dout^T
+            // dH2^T = W3^T dout^T over head rows 0..15 (dout rows 16..31 are zero)
+            fwd_tiles<1, kDp, 1>(W3T, kOut, ft0 + j, D, acc, lane);
             gate_in_place(acc, ft0 + j, H2, lane);
         }
         STAMP(9);
         __syncthreads();
         STAMP(10);
 
-        // ---- dH2 -> HBM (Y of the dW2 GEMM), db2 += column sums of dH2,
+        // ---- db2 column sums of dH2, stage 1: wave w sums rows w * kTR / kFW.. for the 4 columns
+        //      4 lane..; the per-wave sums go to the (dead) dout region, stage 2 follows in dW1.
         //      dH1 = (dH2 W2) * (1 - H1^2)  (wave w: L2 inputs of its tiles, rows = samples)
-#pragma unroll 4
-        for (int c = tid; c < kTR * (kH / 8); c += kFThreads) {
-            const int row = c >> 5, col = 8 * (c & 31);
-            const int64_t m = m0 + row;
-            if (m < p.rows && !(p.diag & 1))
-                *reinterpret_cast<bf16x8*>(p.dh2_out + m * kH + col) = *reinterpret_cast<const bf16x8*>(H2 + row * kHp + col);
-        }
         {
-            constexpr int kRowsPer = kTR * kH / kFThreads;  // rows of one column per thread per tile
-            const int col = tid & (kH - 1), r0 = (tid / kH) * kRowsPer;
-            float sc = 0.0f;  // padding rows carry dH2 = 0 (their dout is 0)
-#pragma unroll 8
-            for (int rr = 0; rr < kRowsPer; ++rr) sc += from_bf16(H2[(r0 + rr) * kHp + col]);
-            db2 += sc;
+            constexpr int kRows = kTR / kFW;
+            float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);  // padding rows carry dH2 = 0 (their dout is 0)
+            const bf16* hp = H2 + (kRows * wave) * kHp + 4 * lane;
+#pragma unroll
+            for (int rr = 0; rr < kRows; ++rr) {
+                const bf16x4 v = *reinterpret_cast<const bf16x4*>(hp + rr * kHp);
+                cs.x += from_bf16(v[0]);
+                cs.y += from_bf16(v[1]);
+                cs.z += from_bf16(v[2]);
+                cs.w += from_bf16(v[3]);
+            }
+            reinterpret_cast<float4*>(lds + kOffD)[wave * 64 + lane] = cs;
         }
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
@@ -474,17 +543,27 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
         // ---- dW1 += dH1^T X (wave w: hidden rows of its tiles, input columns 0..63); LDS only,
         //      so the next tile's X loads go out now
         if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
+        // dH2 tile -> HBM (Y of the dW2 GEMM; H2 holds dH2 until the next tile's L2)
+        copy_tile_out_n<kFThreads>(H2, p.dh2_out, kH, m0, p.rows, tid, p.diag);
+        if (tid < kH) {  // db2 stage 2: the kFW row-group sums of column tid, in row order
+            const float* cs = reinterpret_cast<const float*>(lds + kOffD);
 #pragma unroll
-        for (int kk = 0; kk < kTR; kk += 16) {
-            bf16x8 b[2];
+            for (int w = 0; w < kFW; ++w) db2 += cs[w * kH + tid_l];
+        }
 #pragma unroll
-            for (int it = 0; it < 2; ++it) b[it] = tr_frag<kXp>(X, 32 * it, kk, lane);
+        for (int kk = 0; kk < kTR; kk += 32) {
+            bf16x8 b[3];
 #pragma unroll
-            for (int j = 0; j < kNT; ++j) {
-                const bf16x8 a = tr_frag<kHp>(H1, 32 * (ft0 + j), kk, lane);
+            for (int ci = 0; ci < 3; ++ci) b[ci] = tr_frag16<kXp>(X, 16 * ci, kk, lane);
 #pragma unroll
-                for (int it = 0; it < 2; ++it) if (!(p.diag & 4)) acc1[j][it] = mfma32(a, b[it], acc1[j][it]);
-            }
+            for (int j = 0; j < kNT; ++j)
+#pragma unroll
+                for (int ri = 0; ri < 2; ++ri) {
+                    const bf16x8 a = tr_frag16<kHp>(H1, 32 * (ft0 + j) + 16 * ri, kk, lane);
+#pragma unroll
+                    for (int ci = 0; ci < 3; ++ci)
+                        if (!(p.diag & 4)) acc1[j][ri][ci] = mfma16(a, b[ci], acc1[j][ri][ci]);
+                }
         }
         STAMP(13);
         __syncthreads();
@@ -499,18 +578,25 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
 
     // ---- workgroup partials (fixed layout; summed in a fixed order by launch_slab_reduce)
     float* part = p.part + (int64_t)blockIdx.x * kPartSize;
+    {
+        const int c16 = lane & 15, g16 = lane >> 4;
 #pragma unroll
-    for (int j = 0; j < kNT; ++j)
+        for (int j = 0; j < kNT; ++j)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int o = acc_row(q, lane);
-            part[kPartW3 + o * kHx + 32 * (ft0 + j) + r] = acc3[j][q];
+            for (int i = 0; i < 4; ++i) {
+                const int o = 4 * g16 + i;  // head row (rows 16..31 stay zero: k_fused_scatter)
 #pragma unroll
-            for (int it = 0; it < 2; ++it) part[kPartW1 + (32 * (ft0 + j) + o) * kIn + 32 * it + r] = acc1[j][it][q];
-        }
-    // db2 halves (4 waves: one 128-row half per thread, the other half slot is zero)
-    part[kPartB2 + tid] = db2;
-    if (kFThreads == kH) part[kPartB2 + kH + tid] = 0.0f;
+                for (int ci = 0; ci < 2; ++ci) part[kPartW3 + o * kHx + 32 * (ft0 + j) + 16 * ci + c16] = acc3[j][ci][i];
+#pragma unroll
+                for (int ri = 0; ri < 2; ++ri) {
+                    float* row = part + kPartW1 + (32 * (ft0 + j) + 16 * ri + o) * kIn;
+#pragma unroll
+                    for (int ci = 0; ci < 3; ++ci) row[16 * ci + c16] = acc1[j][ri][ci][i];
+                    row[48 + c16] = 0.0f;  // input columns 48..63: X is zero there
+                }
+            }
+    }
+    if (tid < kH) part[kPartB2 + tid] = db2;
     float* red = reinterpret_cast<float*>(lds);              // [head lanes][16]
     double* lred = reinterpret_cast<double*>(lds + kOffH1);  // [head lanes][4]
     if (wave < kHW) {
@@ -520,7 +606,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
             red[tid * 16 + 8 + q] = db3[q];
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) lred[tid * 4 + k] = lsum[k];
+        for (int k = 0; k < 4; ++k) lred[tid * 4 + k] = (double)lsum[k];
     }
     __syncthreads();
     if (tid < 32) {  // head row o: lanes with h = (o >> 2) & 1, register q = (o & 3) + 4 (o >> 3)
@@ -552,13 +638,14 @@ __global__ void k_fused_scatter(const float* __restrict__ sum, float* __restrict
     if (j >= kPartB2) {  // W2 block column 256 (bias) and the zero pad columns 257..287 of row n
         const int n = j - kPartB2;
         if (n < kH) {
-            gW2[(int64_t)n * kHx + kH] = sum[kPartB2 + n] + sum[kPartB2 + kH + n];
+            gW2[(int64_t)n * kHx + kH] = sum[kPartB2 + n];
             for (int c = kH + 1; c < kHx; ++c) gW2[(int64_t)n * kHx + c] = 0.0f;
         }
         return;
     }
-    const int col = (j - kPartW3) % kHx;
-    const bool w3pad = j >= kPartW3 && j < kPartLs && col > kH;  // never written by k_pg_fused
+    const int col = (j - kPartW3) % kHx, orow = (j - kPartW3) / kHx;
+    // never written by k_pg_fused: the pad columns 257.. and the dW3 rows 16..31 but their bias column
+    const bool w3pad = j >= kPartW3 && j < kPartLs && (col > kH || (orow >= 16 && col < kH));
     const float s = w3pad ? 0.0f : sum[j];
     if (j < kPartW3) gW1[j] = s;
     else if (j < kPartLs) gW3[j - kPartW3] = s;

@@ -93,7 +93,7 @@ class PgFusedArgs(C.Structure):
                [(k, C.c_double) for k in ("inv_total_samples", "clip_eps", "vf_coef", "ent_coef")] + \
                [(k, C.c_void_p) for k in ("values", "h1", "dh2", "partial", "loss_partial")] + \
                [("grid", C.c_int32), ("wgrad_splits", C.c_int32), ("wgrad_partial", C.c_void_p),
-                ("grads", C.c_void_p)]
+                ("grads", C.c_void_p), ("h1_mode", C.c_int32)]
 
 
 _P = C.c_void_p

@@ -42,5 +42,10 @@ int launch_slab_reduce(const float* partial, int64_t slab, int z, float* tmp, fl
 // [splits + kReduceGroups][O][I]).
 int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, int I, int64_t M, int splits,
                  float* partial, float* out, hipStream_t st, int64_t ldo = 0);
+// out[256][ldo] = sum_m Y[m][o] tanh(obs[m] . W1^T)[i] for the 256-wide first hidden layer of the
+// actor-critic MLP (obs [M][ldobs] bf16, 64 used columns; W1 [256][64]); H1 is recomputed on chip
+// exactly as the fused learner's forward computes it.  M % 32 == 0; partial as launch_wgrad.
+int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, const bf16* W1, int64_t M,
+                    int splits, float* partial, float* out, hipStream_t st, int64_t ldo);
 
 }  // namespace dxrl

@@ -253,6 +253,7 @@ struct WgradArgs {
     float* partial;  // [splits][O][I] (splits > 1)
     int64_t ldo;     // output row stride (>= I)
     int diag;        // timing ablation (DXRL_WGRAD_DIAG): 1 = stream only, no fragment reads / MFMAs
+    const bf16* W1;  // k_wgrad_l1: [256][64] first-layer weights (X is then the observation matrix)
 };
 
 __global__ __launch_bounds__(256) void k_wgrad_bf16(WgradArgs w) {
@@ -568,6 +569,208 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_glds(WgradArgs w) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) dst[(int64_t)(32 * wave + acc_row(q, lane)) * ld + i] = acc[j][q];
     }
+}
+
+// k_wgrad_l1: dW2 = dH2^T H1 without H1 in HBM.  H1 = tanh(obs W1^T) is recomputed per 32-sample
+// chunk from the 128-byte observation rows (a quarter of H1's bytes) with exactly the fused
+// learner's L1 sequence -- same MFMA, operand roles, k order and tanh -- so the bf16 H1 is bit for
+// bit the one the learner's forward used (test_h1_recompute_is_bit_exact).  The chunk ring is
+// k_wgrad_glds's (dH2 rows 512 B, source-swizzled by 4 (r & 3)); observation rows land 128 B
+// unpadded with their 16-byte chunks swizzled by (r >> 1) & 7, which keeps the row-fragment reads
+// conflict-free.  Each wave issues three LDS-DMA ops per chunk (two dH2 pieces of 2 rows, one
+// half-wave piece of 4 observation rows).  Software-pipelined by one chunk: iteration c recomputes
+// H1(c + 1) into one of two H1 buffers while contracting chunk c against the other, one barrier per
+// chunk; the H1(c + 1) products sit between the two k-steps of chunk c in the MFMA pipe, so their
+// tanh issues on the VALU while the second k-step runs on the matrix cores.
+constexpr int kLK = 32, kLNB = 5;
+constexpr int kLYB = kLK * 512, kLXB = kLK * 128, kLSlot = kLYB + kLXB;
+constexpr int kLH1 = kLNB * kLSlot;          // two recomputed H1 chunks [32][256] (h1_swz rows)
+constexpr int kLLds = kLH1 + 2 * kLK * 512;  // 132 KiB
+
+__device__ __forceinline__ void glds_x4(const void* src, const void* lds_dst) {
+    const uint32_t lds_addr =
+        __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds_dst);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_addr)
+                 : "memory");
+}
+
+// H1 chunk layout: 512-B rows, 16-byte chunk c of row r at c ^ (4 (r & 3) ^ ((r >> 2) & 3)).  The
+// 4 (r & 3) term keeps the transposed reads conflict-free (as tr_frag_swz); the (r >> 2) & 3 term
+// spreads the 16 rows of one ds_write_b64 lane group over 8 chunk slots (2-way, not 8-way).
+__device__ __forceinline__ int h1_swz(int row) { return (4 * (row & 3)) ^ ((row >> 2) & 3); }
+__device__ __forceinline__ bf16x8 tr_frag_h1(const bf16* tile, int col0, int kk, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int col = col0 + 16 * (g & 1) + 4 * p;
+    lds_bf16* base = (lds_bf16*)(tile);
+    const auto at = [&](int row) {
+        return (lds_bf16x4*)(base + row * 256 + (((col >> 3) ^ h1_swz(row)) << 3) + (col & 7));
+    };
+    const int row = kk + 8 * (g >> 1) + q;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(at(row));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(at(row + 4));
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = lo[j];
+        v[4 + j] = hi[j];
+    }
+    return v;
+}
+
+// s_waitcnt vmcnt(3 n) (n = 0..3 chunks of three LDS-DMA ops each still in flight)
+__device__ __forceinline__ void wait_chunks(int n) {
+    if (n >= 3) __builtin_amdgcn_s_waitcnt(0xF79);
+    else if (n == 2) __builtin_amdgcn_s_waitcnt(0xF76);
+    else if (n == 1) __builtin_amdgcn_s_waitcnt(0xF73);
+    else __builtin_amdgcn_s_waitcnt(0xF70);
+}
+
+__global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
+    extern __shared__ __attribute__((aligned(16))) char gsm[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t total = w.M / kLK;
+    const int nch = (int)((total - blockIdx.x + gridDim.x - 1) / gridDim.x);
+    const bf16* const Y = w.Y;
+    const bf16* const X = w.X;
+    const int64_t ldy = w.ldy, ldx = w.ldx;
+    f32x16 acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[j][q] = 0.0f;
+    // this wave's 32 hidden units of W1 (A operand of the recompute), register-resident
+    bf16x8 w1f[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        w1f[k] = *(const __attribute__((address_space(1))) bf16x8*)(w.W1 + (32 * wave + r) * 64 + 16 * k + 8 * h);
+    const auto issue = [&](int c) {
+        char* slot = gsm + (c % kLNB) * kLSlot;
+        const int64_t m0 = ((int64_t)blockIdx.x + (int64_t)c * gridDim.x) * kLK;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // dH2 rows 4 wave + 2 i, + 1
+            const int prow = 4 * wave + 2 * i;
+            const int rr = prow + (lane >> 5), gchunk = (lane & 31) ^ (4 * (rr & 3));
+            glds_x4(Y + (m0 + rr) * ldy + 8 * gchunk, slot + prow * 512);
+        }
+        if (lane < 32) {  // observation rows 4 wave .. + 3
+            const int row = 4 * wave + (lane >> 3), pc = (lane & 7) ^ ((row >> 1) & 7);
+            glds_x4(X + (m0 + row) * ldx + 8 * pc, slot + kLYB + 512 * wave);
+        }
+    };
+    // H1[32 samples][hidden 32 wave ..] of chunk c = tanh(obs W1^T): the fused learner's L1, one tile
+    // (products and tanh split so the caller can put MFMA work between them)
+    const auto recompute_mfma = [&](int c, f32x16& ha) {
+        const bf16* Os = (const bf16*)(gsm + (c % kLNB) * kLSlot + kLYB);
+        bf16x8 b[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) b[k] = *reinterpret_cast<const bf16x8*>(Os + r * 64 + 8 * ((2 * k + h) ^ ((r >> 1) & 7)));
+#pragma unroll
+        for (int q = 0; q < 16; ++q) ha[q] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ha = mfma32(w1f[k], b[k], ha);
+    };
+    const auto recompute_store = [&](int c, const f32x16& ha) {
+        bf16* H1 = (bf16*)(gsm + kLH1 + (c & 1) * kLK * 512);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f0 = 32 * wave + 8 * g + 4 * h;
+            bf16x4 v;
+#pragma unroll
+            for (int u = 0; u < 4; u += 2) {
+                const f32x2 t = tanh_pre2(f32x2{ha[4 * g + u], ha[4 * g + u + 1]}, f32x2{0.0f, 0.0f});
+                v[u] = to_bf16(t.x);
+                v[u + 1] = to_bf16(t.y);
+            }
+            *reinterpret_cast<bf16x4*>(H1 + r * 256 + (((f0 >> 3) ^ h1_swz(r)) << 3) + (f0 & 7)) = v;
+        }
+    };
+    // dW2 += dH2(c)^T H1(c), k-step hh (16 samples)
+    const auto contract = [&](int c, int hh) {
+        const bf16* Ys = (const bf16*)(gsm + (c % kLNB) * kLSlot);
+        const bf16* H1 = (const bf16*)(gsm + kLH1 + (c & 1) * kLK * 512);
+        bf16x8 bb[8];
+        const bf16x8 a = tr_frag_swz(Ys, 32 * wave, 16 * hh, lane);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bb[j] = tr_frag_h1(H1, 32 * j, 16 * hh, lane);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = mfma32(a, bb[j], acc[j]);
+    };
+    constexpr int kLead = kLNB - 1;  // chunks in flight ahead of the one being contracted
+#pragma unroll
+    for (int c = 0; c < kLead; ++c)
+        if (c < nch) issue(c);
+    if (nch > 0) {
+        wait_chunks(min(kLead - 1, nch - 1));  // chunk 0 in
+        __builtin_amdgcn_s_barrier();
+        f32x16 ha;
+        recompute_mfma(0, ha);
+        recompute_store(0, ha);
+    }
+    for (int c = 0; c < nch; ++c) {
+        // chunk c + 1 in (chunks c + 2 .. c + kLead - 1 may still fly); H1(c) complete; chunk c - 1 done
+        wait_chunks(max(0, min(kLead - 2, nch - 2 - c)));
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (c + kLead < nch) issue(c + kLead);  // into the slot chunk c - 1 released
+        const bool next = c + 1 < nch && !(w.diag & 2), mm = !(w.diag & 1);
+        if (mm) contract(c, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        f32x16 ha;
+        if (next) recompute_mfma(c + 1, ha);
+        __builtin_amdgcn_sched_barrier(0);
+        if (mm) contract(c, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (next) recompute_store(c + 1, ha);
+    }
+    float* dst = w.partial ? w.partial + (int64_t)blockIdx.x * 256 * 256 : w.out;
+    const int64_t ld = w.partial ? 256 : w.ldo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int i = 32 * j + (lane & 31);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dst[(int64_t)(32 * wave + acc_row(q, lane)) * ld + i] = acc[j][q];
+    }
+}
+
+int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, const bf16* W1, int64_t M,
+                    int splits, float* partial, float* out, hipStream_t st, int64_t ldo) {
+    DXRL_REQUIRE(Y && obs && W1 && out && M > 0 && M % kLK == 0, "wgrad_l1: M must be a positive multiple of %d", kLK);
+    DXRL_REQUIRE(ldy >= 256 && ldy % 8 == 0 && ldobs >= 64 && ldobs % 8 == 0 && ldo >= 256, "wgrad_l1: bad strides");
+    if (splits < 1) splits = 1;
+    if (splits > M / kLK) splits = (int)(M / kLK);
+    if (splits > 1) DXRL_REQUIRE(partial, "wgrad_l1: split-K needs a partial slab");
+    WgradArgs w{};
+    w.Y = Y;
+    w.ldy = ldy;
+    w.X = obs;
+    w.ldx = ldobs;
+    w.W1 = W1;
+    w.O = 256;
+    w.I = 256;
+    w.M = M;
+    w.out = out;
+    w.partial = splits > 1 ? partial : nullptr;
+    w.ldo = ldo;
+    static bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(k_wgrad_l1),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLLds) == hipSuccess;
+    }();
+    DXRL_REQUIRE(attr, "wgrad_l1: could not raise the dynamic LDS limit");
+    static const int diag = [] {
+        const char* v = getenv("DXRL_WGRAD_DIAG");
+        return v ? atoi(v) : 0;
+    }();
+    w.diag = diag;
+    hipLaunchKernelGGL(k_wgrad_l1, dim3((unsigned)splits), dim3(512), kLLds, st, w);
+    if (int rc = launch_check("k_wgrad_l1")) return rc;
+    if (splits > 1) {
+        const int64_t slab = 256 * 256;
+        return launch_slab_reduce(partial, slab, splits, partial + (int64_t)splits * slab, out, 0, st, 256, ldo);
+    }
+    return DXRL_OK;
 }
 
 // out[i] (+)= sum_z partial[z][i], fixed order (deterministic)

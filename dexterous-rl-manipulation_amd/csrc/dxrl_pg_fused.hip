@@ -368,7 +368,8 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
         // H1 tile -> HBM (B operand of the dW2 GEMM) by the waves that have no head tile; their
         // stores then retire while the head runs instead of holding the head's load waits
         if constexpr (kTrain && kFW > kHW) {
-            if (wave >= kHW) copy_tile_out_n<64 * (kFW - kHW)>(H1, p.h1_out, kHx, m0, p.rows, tid - 64 * kHW, p.diag);
+            if (wave >= kHW && p.h1_out)
+                copy_tile_out_n<64 * (kFW - kHW)>(H1, p.h1_out, kHx, m0, p.rows, tid - 64 * kHW, p.diag);
         }
         if (wave < kHW) {
             f32x16 acc;
@@ -486,7 +487,9 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
             STAMP(7);
             continue;
         }
-        if constexpr (kFW == kHW) copy_tile_out_n<kFThreads>(H1, p.h1_out, kHx, m0, p.rows, tid, p.diag);
+        if constexpr (kFW == kHW) {
+            if (p.h1_out) copy_tile_out_n<kFThreads>(H1, p.h1_out, kHx, m0, p.rows, tid, p.diag);
+        }
         STAMP(7);
         __syncthreads();
         STAMP(8);
@@ -675,7 +678,8 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     const bool train = a->train != 0;
     if (!train) DXRL_REQUIRE(a->net == 1 && a->values, "fused: forward mode computes critic values only");
     if (train) {
-        DXRL_REQUIRE(a->h1 && a->dh2 && a->partial && a->loss_partial && a->grads && a->wgrad_partial &&
+        DXRL_REQUIRE(a->h1_mode == 0 || a->h1_mode == 1, "fused: h1_mode must be 0 or 1");
+        DXRL_REQUIRE((a->h1 || (a->h1_mode == 0 && a->rows % 32 == 0)) && a->dh2 && a->partial && a->loss_partial && a->grads && a->wgrad_partial &&
                          a->wgrad_splits >= 1,
                      "fused: training needs h1/dh2 scratch, partial slabs and grads");
         DXRL_REQUIRE(a->net == 1 ? (a->ret != nullptr) : (a->act && a->logp_old && a->adv && a->stats),
@@ -710,7 +714,10 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     f.clip_eps = (float)a->clip_eps;
     f.vf2 = (float)(2.0 * a->vf_coef);
     f.v_out = a->values;
-    f.h1_out = static_cast<bf16*>(a->h1);
+    // H1 reaches the dW2 contraction either recomputed on chip from the observations
+    // (launch_wgrad_l1: rows % 32 == 0) or as an HBM copy written by this kernel
+    const bool recompute = train && a->rows % 32 == 0 && a->h1_mode == 0;
+    f.h1_out = recompute ? nullptr : static_cast<bf16*>(a->h1);
     f.dh2_out = static_cast<bf16*>(a->dh2);
     f.part = a->partial;
     f.loss = a->loss_partial;
@@ -754,6 +761,9 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
                        G + (c ? kOffW1c : kOffW1a), G + o3, c ? nullptr : G + kOffLogStd, G + o2, (float)a->ent_coef);
     if (int rc = launch_check("k_fused_scatter")) return rc;
     // dW2[:, 0..255] = dH2^T H1 (the bias column 256 came from the column sums above)
+    if (recompute)
+        return launch_wgrad_l1(static_cast<const bf16*>(a->dh2), kH, f.X, kIn, f.W1, a->rows, a->wgrad_splits,
+                               a->wgrad_partial, G + o2, st, kHx);
     return launch_wgrad(static_cast<const bf16*>(a->dh2), kH, kH, static_cast<const bf16*>(a->h1), kHx, kH, a->rows,
                         a->wgrad_splits, a->wgrad_partial, G + o2, st, kHx);
 }

@@ -72,6 +72,7 @@ class TrainerConfig:
     seed: int = 0
     splitk_target_blocks: int = 768
     fused: bool = True                       # one-pass learner kernels (dxrl_pg_fused) vs the GEMM chain
+    h1_recompute: bool = True                # fused dW2: recompute H1 from obs on chip (no H1 HBM round trip)
     record_cap: int = 0                      # per-env episode records per iteration (0 = off)
     success_rule: str = "terminated"         # "training" (episode_utils.py:52) or "terminated"
 
@@ -233,6 +234,7 @@ class PGTrainer:
         f.h1, f.dh2 = p(self.H1a), p(self.dH2)
         f.partial, f.loss_partial, f.grid = p(self.fused_partial), p(self.fused_loss), self.fused_grid
         f.wgrad_splits, f.wgrad_partial, f.grads = self.splits, p(self.kpartial), p(self.grads)
+        f.h1_mode = 0 if c.h1_recompute else 1
         return f
 
     def critic_values(self):

@@ -298,7 +298,10 @@ int dxrl_pg_adam(int32_t device, float* params, const float* grads, float* m1, f
  * One launch per network replaces forward GEMMs + heads + backward GEMMs of the
  * layer-by-layer path (dxrl_gemm_bf16 / dxrl_pg_heads / dxrl_wgrad_bf16): per
  * 128-sample tile it runs the MLP forward, the PPO-clip (actor) or value (critic)
- * head and the backward pass out of LDS, then dW2 = dH2^T [H1 | 1] by split-K.
+ * head and the backward pass out of LDS (db2 as fused column sums of dH2), then
+ * dW2 = dH2^T H1 as one split-K contraction over dH2 (HBM).  H1 reaches it either
+ * recomputed on chip from obs (h1_mode 0, rows % 32 == 0: no H1 traffic at all) or as
+ * the h1 scratch copy this launch writes (h1_mode 1, or rows % 32 != 0).
  * train == 0 (critic only): forward pass writing values[rows] (GAE bootstrap pass). */
 typedef struct dxrl_pg_fused_args {
     int32_t net;               /* 0 actor, 1 critic                                        */
@@ -315,7 +318,7 @@ typedef struct dxrl_pg_fused_args {
     double inv_total_samples;  /* 1 / (samples summed over ranks)                          */
     double clip_eps, vf_coef, ent_coef;
     float* values;             /* forward mode: f32 [rows]                                 */
-    void* h1;                  /* bf16 [rows][288] scratch, column 256 preset to 1         */
+    void* h1;                  /* bf16 [rows][288] scratch (used by the H1 copy mode only)  */
     void* dh2;                 /* bf16 [rows][256] scratch                                 */
     float* partial;            /* f32 [grid + 17][dxrl_pg_fused_sizes().partial_floats]    */
     double* loss_partial;      /* f64 [grid][4]: actor writes 0,2,3, critic writes 1       */
@@ -323,6 +326,7 @@ typedef struct dxrl_pg_fused_args {
     int32_t wgrad_splits;      /* split-K factor of the dW2 GEMM                           */
     float* wgrad_partial;      /* f32 [wgrad_splits + 16][256][288]                        */
     float* grads;              /* f32 master-layout gradients: W1/W2/W3 (+ log_std) blocks */
+    int32_t h1_mode;           /* 0 recompute H1 for dW2 when rows % 32 == 0, 1 HBM copy    */
 } dxrl_pg_fused_args;
 
 int dxrl_pg_fused_sizes(int32_t* tile_rows, int64_t* partial_floats_per_block);

@@ -131,13 +131,15 @@ def test_iteration_matches_torch_reference(pkg, fused):
     assert M == tr.M
 
 
-@pytest.mark.parametrize("n,T", [(256, 32), (96, 33)])  # 96 * 33 = 3168: ragged last 128-sample tile
-def test_fused_learner_matches_gemm_chain(pkg, n, T):
+@pytest.mark.parametrize("n,T,h1_recompute", [(256, 32, True), (96, 33, True), (256, 32, False), (96, 33, False)])
+def test_fused_learner_matches_gemm_chain(pkg, n, T, h1_recompute):
     """dxrl_pg_fused (one pass per network) == the layer-by-layer GEMM chain: same bf16
-    storage points, so only f32 accumulation order differs."""
+    storage points, so only f32 accumulation order differs (96 * 33 = 3168: ragged last
+    128-sample tile).  h1_recompute: dW2 with H1 recomputed from obs on chip vs read back
+    from the HBM copy."""
     if (n * T) % 32:
         pytest.skip("trainer needs num_envs * horizon % 32 == 0")
-    _, tf = make(pkg, n, T, fused=True)
+    _, tf = make(pkg, n, T, fused=True, h1_recompute=h1_recompute)
     _, tu = make(pkg, n, T, fused=False)
     tf.rollout()
     tu.rollout()
@@ -161,6 +163,21 @@ def test_fused_learner_matches_gemm_chain(pkg, n, T):
     lf, lu = tf.loss_stats(), tu.loss_stats()
     for k in ("policy_loss", "value_mse", "clip_frac", "approx_kl"):
         assert math.isclose(lf[k], lu[k], rel_tol=1e-4, abs_tol=1e-7), (k, lf[k], lu[k])
+
+
+def test_h1_recompute_is_bit_exact(pkg):
+    """dW2 from H1 recomputed on chip (k_wgrad_l1) == dW2 from the H1 HBM copy, bit for bit:
+    the recompute repeats the learner forward's L1 exactly and both contractions sum in the
+    same order."""
+    grads = []
+    for rec in (True, False):
+        _, tr = make(pkg, 256, 32, fused=True, h1_recompute=rec)
+        tr.rollout()
+        for name in [x for x in tr.phases() if x not in ("rollout", "optimizer_step")]:
+            getattr(tr, name)()
+        torch.cuda.synchronize()
+        grads.append(tr.grads.clone())
+    assert torch.equal(grads[0], grads[1])
 
 
 def test_adam_matches_manual(pkg):

@@ -785,37 +785,98 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
 
 // ------------------------------------------------------------------ GAE
 // delta_t = r_t + gamma V_{t+1} (1 - d_t) - V_t ; A_t = delta_t + gamma lambda (1 - d_t) A_{t+1}
-// One thread per env scans t = T-1 .. 0 (coalesced across envs).  Block
-// partial sums of A for the normalisation's first pass.
-__global__ void k_gae(const float* __restrict__ rew, const uint8_t* __restrict__ done, const float* __restrict__ V,
-                      int64_t n, int64_t T, float gamma, float lam, float* __restrict__ adv, float* __restrict__ ret,
-                      double* __restrict__ partial) {
-    __shared__ double red[256];
+// One thread per env scans t = T-1 .. 0 (coalesced across envs), 64-env workgroups so the scan
+// spreads over 64 CUs.  The loads of kGaeChunk steps go out together before that chunk's
+// recurrence runs (one HBM latency per chunk, not per step).  Block partials of sum A and
+// sum A^2 (f64) for the normalisation: partial[b] and partial[nb + b].
+constexpr int kGaeChunk = 32, kGaeThreads = 64;
+__global__ __launch_bounds__(kGaeThreads) void k_gae(const float* __restrict__ rew, const uint8_t* __restrict__ done,
+                                                     const float* __restrict__ V, int64_t n, int64_t T, float gamma,
+                                                     float lam, float* __restrict__ adv, float* __restrict__ ret,
+                                                     double* __restrict__ partial) {
+    __shared__ double red[2][kGaeThreads];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    double s = 0.0;
-    if (i < n) {
-        float next_adv = 0.0f;
-        float next_v = V[T * n + i];
-        for (int64_t t = T - 1; t >= 0; --t) {
-            const int64_t m = t * n + i;
-            const float nd = done[m] ? 0.0f : 1.0f;
-            const float v = V[m];
-            const float delta = rew[m] + gamma * next_v * nd - v;
+    const int64_t ic = i < n ? i : n - 1;  // clamped: every lane loads, only real envs store
+    double s = 0.0, s2 = 0.0;
+    float next_adv = 0.0f;
+    float next_v = V[T * n + ic];
+    for (int64_t hi = T; hi > 0; hi -= kGaeChunk) {
+        const int64_t lo = hi - kGaeChunk > 0 ? hi - kGaeChunk : 0;
+        float rv[kGaeChunk], vv[kGaeChunk];
+        uint8_t dv[kGaeChunk];
+#pragma unroll
+        for (int k = 0; k < kGaeChunk; ++k) {
+            const int64_t t = lo + k < hi ? lo + k : hi - 1;
+            const int64_t m = t * n + ic;
+            rv[k] = rew[m];
+            vv[k] = V[m];
+            dv[k] = done[m];
+        }
+#pragma unroll
+        for (int k = kGaeChunk - 1; k >= 0; --k) {
+            if (lo + k >= hi) continue;
+            const float nd = dv[k] ? 0.0f : 1.0f;
+            const float delta = rv[k] + gamma * next_v * nd - vv[k];
             const float a = delta + gamma * lam * nd * next_adv;
-            adv[m] = a;
-            ret[m] = a + v;
-            s += a;
+            const int64_t m = (lo + k) * n + ic;
+            if (i < n) {
+                adv[m] = a;
+                ret[m] = a + vv[k];
+                s += a;
+                s2 += (double)a * (double)a;
+            }
             next_adv = a;
-            next_v = v;
+            next_v = vv[k];
         }
     }
-    red[threadIdx.x] = s;
+    red[0][threadIdx.x] = s;
+    red[1][threadIdx.x] = s2;
     __syncthreads();
     for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        if (threadIdx.x < w) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + w];
+            red[1][threadIdx.x] += red[1][threadIdx.x + w];
+        }
         __syncthreads();
     }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    if (threadIdx.x == 0) {
+        partial[blockIdx.x] = red[0][0];
+        partial[gridDim.x + blockIdx.x] = red[1][0];
+    }
+}
+
+// stats[0] = count, stats[1] = sum (partial[0..nb)), stats[3] = sum of squares (partial[nb..2 nb))
+__global__ void k_gae_sums(const double* __restrict__ partial, int nb, double count, double* __restrict__ stats) {
+    __shared__ double red[2][256];
+    double s = 0.0, s2 = 0.0;
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) {
+        s += partial[k];
+        s2 += partial[nb + k];
+    }
+    red[0][threadIdx.x] = s;
+    red[1][threadIdx.x] = s2;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + w];
+            red[1][threadIdx.x] += red[1][threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        stats[0] = count;
+        stats[1] = red[0][0];
+        stats[3] = red[1][0];
+    }
+}
+
+// one-pass finalisation from global count / sum / sum of squares: mean, sum sq dev, unbiased std
+__global__ void k_stats_onepass(double* stats) {
+    const double c = stats[0], mean = stats[1] / c;
+    const double ssd = fmax(stats[3] - mean * stats[1], 0.0);
+    stats[2] = mean;
+    stats[3] = ssd;
+    stats[4] = sqrt(ssd / (c > 1.0 ? c - 1.0 : 1.0));
 }
 
 // block partials of sum (x - center)^2 (second pass of the normalisation)
@@ -1138,11 +1199,12 @@ int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const flo
     DXRL_REQUIRE(rew && done && values && adv && ret && partial && stats, "null argument");
     DeviceGuard g(device);
     hipStream_t st = as_stream(stream);
-    const int nb = (int)((num_envs + 255) / 256);
-    hipLaunchKernelGGL(k_gae, dim3(nb), dim3(256), 0, st, rew, done, values, num_envs, horizon, (float)gamma,
+    const int nb = (int)((num_envs + kGaeThreads - 1) / kGaeThreads);
+    hipLaunchKernelGGL(k_gae, dim3(nb), dim3(kGaeThreads), 0, st, rew, done, values, num_envs, horizon, (float)gamma,
                        (float)lam, adv, ret, partial);
     if (int rc = launch_check("k_gae")) return rc;
-    return reduce_to(partial, nb, stats, 1, st);
+    hipLaunchKernelGGL(k_gae_sums, dim3(1), dim3(256), 0, st, partial, nb, (double)(num_envs * horizon), stats);
+    return launch_check("k_gae_sums");
 }
 
 int dxrl_pg_adv_finalize(int32_t device, int32_t phase, const float* adv, int64_t count, double* partial,
@@ -1157,6 +1219,10 @@ int dxrl_pg_adv_finalize(int32_t device, int32_t phase, const float* adv, int64_
         hipLaunchKernelGGL(k_sqdev, dim3(nb), dim3(256), 0, st, adv, count, stats, partial);
         if (int rc = launch_check("k_sqdev")) return rc;
         return reduce_to(partial, nb, stats, 3, st);
+    }
+    if (phase == 2) {  // one pass: stats[0] count, [1] sum, [3] sum of squares are global
+        hipLaunchKernelGGL(k_stats_onepass, dim3(1), dim3(1), 0, st, stats);
+        return launch_check("k_stats_onepass");
     }
     hipLaunchKernelGGL(k_stats_std, dim3(1), dim3(1), 0, st, stats);
     return launch_check("k_stats_std");

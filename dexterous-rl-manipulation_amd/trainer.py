@@ -9,7 +9,7 @@ actor-critic with GAE and policy gradients on top of the same env.  One
      the step kernel (bf16 MFMA), Gaussian sampling, optional fused noise
      injection (robustness_tests.py:140-211), auto-reset, training tape;
   2. critic forward over the T+1 observation blocks (bf16 MFMA GEMMs);
-  3. ``dxrl_pg_gae`` reverse scan + two-pass advantage normalisation
+  3. ``dxrl_pg_gae`` reverse scan + one-pass (f64 moments) advantage normalisation
      (global across ranks: two 1-element all-reduces);
   4. actor forward, PPO-clip / value / entropy heads (``dxrl_pg_heads``);
   5. backward GEMMs (input grads with fused tanh' gate, weight grads by
@@ -131,7 +131,7 @@ class PGTrainer:
         self.V = z(OUT, (T + 1) * n)
         self.adv, self.ret = z(M), z(M)
         self.stats = torch.zeros(8, dtype=torch.float64, device=d)
-        nb = max(1024, (M + 255) // 256, (n + 255) // 256)
+        nb = max(1024, (M + 255) // 256, 2 * ((n + 63) // 64))  # GAE: 2 moments per 64-env block
         self.partial = torch.zeros(nb, dtype=torch.float64, device=d)
         self.dmu_rm, self.dv_rm = z(M, OUT, dt=bf), z(M, OUT, dt=bf)
         self.dls_partial = z((M + 255) // 256, ACT_PAD)
@@ -260,12 +260,9 @@ class PGTrainer:
         c = self.cfg
         N.call("dxrl_pg_gae", self.dev.index, N.ptr(self.rew), N.ptr(self.done), N.ptr(self.V[0]), self.n, self.T,
                c.gamma, c.lam, N.ptr(self.adv), N.ptr(self.ret), N.ptr(self.partial), N.ptr(self.stats), self._s())
-        self.stats[0] = float(self.M)
-        self._allreduce(self.stats[0:2])
-        N.call("dxrl_pg_adv_finalize", self.dev.index, 0, N.ptr(self.adv), self.M, N.ptr(self.partial),
-               N.ptr(self.stats), self._s())
-        self._allreduce(self.stats[3:4])
-        N.call("dxrl_pg_adv_finalize", self.dev.index, 1, N.ptr(self.adv), self.M, N.ptr(self.partial),
+        # count, sum and sum of squares in one all-reduce, then mean / std on device (one pass, f64)
+        self._allreduce(self.stats[0:4])
+        N.call("dxrl_pg_adv_finalize", self.dev.index, 2, N.ptr(self.adv), self.M, N.ptr(self.partial),
                N.ptr(self.stats), self._s())
 
     def heads(self):

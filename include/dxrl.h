@@ -255,13 +255,16 @@ typedef struct dxrl_pg_rollout_args {
 int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, const dxrl_pg_rollout_args* args,
                     void* stream);
 
-/* GAE reverse scan; values f32 [(T+1) N]; writes adv/ret [T N] and stats[1] = local sum(adv). */
+/* GAE reverse scan; values f32 [(T+1) N]; writes adv/ret [T N] and the local moments
+ * stats[0] = T N, stats[1] = sum(adv), stats[3] = sum(adv^2) (partial: f64 [2 ceil(N / 64)]). */
 int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const float* values, int64_t num_envs,
                 int64_t horizon, double gamma, double lam, float* adv, float* ret, double* partial, double* stats,
                 void* stream);
 /* Advantage normalisation, two passes.  phase 0: stats[0] = global count and stats[1] =
  * global sum must be set (all-reduced across ranks) -> mean, stats[3] = local sum sq dev.
- * phase 1 (after all-reducing stats[3]): stats[4] = unbiased std. */
+ * phase 1 (after all-reducing stats[3]): stats[4] = unbiased std.
+ * phase 2 (one pass, after all-reducing stats[0..3] as dxrl_pg_gae left them): mean,
+ * stats[3] = sum sq dev = sum(adv^2) - mean sum(adv), stats[4] = unbiased std. */
 int dxrl_pg_adv_finalize(int32_t device, int32_t phase, const float* adv, int64_t count, double* partial,
                          double* stats, void* stream);
 

@@ -40,17 +40,21 @@ namespace dxrl {
 namespace {
 
 constexpr float kLog2PiF = 1.8378770664093453f;
-constexpr int kTR = 128;                 // samples per tile
 constexpr int kXp = kIn + 8;             // 72:  X rows (conflict-free b128 row reads)
 constexpr int kHp = kH + 8;              // 264: H1 / H2 rows
 constexpr int kDp = kOut + 8;            // 40:  dout rows
-constexpr int kOffX = 0;
-constexpr int kOffH1 = kOffX + kTR * kXp;
-constexpr int kOffH2 = kOffH1 + kTR * kHp;
-constexpr int kOffD = kOffH2 + kTR * kHp;
-constexpr int kLdsElems = kOffD + kTR * kDp;
-static_assert(kLdsElems * 2 == 163840, "the fused kernel uses exactly the CU's 160 KiB of LDS");
-constexpr int kHW = kTR / 32;            // waves running the heads (one 32-sample tile each)
+
+// LDS image of one kTR-sample tile: X [kTR][kXp], H1 / H2 [kTR][kHp], dout [kTR][kDp] (bf16).
+// kTR = 128: 160 KiB, one workgroup per CU; kTR = 64: 80 KiB, two workgroups per CU.
+template <int kTR>
+struct TileLds {
+    static constexpr int kOffX = 0;
+    static constexpr int kOffH1 = kOffX + kTR * kXp;
+    static constexpr int kOffH2 = kOffH1 + kTR * kHp;
+    static constexpr int kOffD = kOffH2 + kTR * kHp;
+    static constexpr int kElems = kOffD + kTR * kDp;
+    static_assert(kElems * 2 * (128 / kTR) == 163840, "one CU's 160 KiB of LDS per 128 samples");
+};
 
 // per-workgroup gradient partial slab (f32)
 constexpr int kPartW1 = 0;                   // [256][64]
@@ -94,20 +98,19 @@ __device__ __forceinline__ void zero_acc(f32x16& a) {
     for (int q = 0; q < 16; ++q) a[q] = 0.0f;
 }
 
-// acc[j][mt] (features 32 (ft0 + j).. x samples 32 mt..) = W[32 (ft0 + j) + r][:] . A[32 mt + r][:]
+// acc[mt] (features 32 ft0.. x samples 32 mt..) = W[32 ft0 + r][:] . A[32 mt + r][:]
 // over KS k-steps.  Weight fragments stream from L2 one 4-k-step chunk ahead (double
-// buffer); each activation fragment read from LDS feeds NT MFMAs.
+// buffer); each weight fragment feeds MT MFMAs.
 struct NoHook {
     __device__ void operator()() const {}
 };
-template <int KS, int kLda, int NT, typename Hook = NoHook>
+template <int KS, int kLda, int MT, typename Hook = NoHook>
 __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int ldw, int ft0, const bf16* A,
-                                          f32x16 (&acc)[NT][4], int lane, Hook hook = Hook{}) {
-    static_assert(NT == 1, "one feature tile per call");
+                                          f32x16 (&acc)[MT], int lane, Hook hook = Hook{}) {
     const int r = lane & 31, h = lane >> 5;
     constexpr int kD = KS < 8 ? KS : 8;  // weight prefetch distance (k-steps)
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) zero_acc(acc[0][mt]);
+    for (int mt = 0; mt < MT; ++mt) zero_acc(acc[mt]);
     // weights through the global address space (global_load: vmcnt only -- a flat load would
     // also hold every LDS wait), kD k-steps ahead
     const gbf16x8* wp = (const gbf16x8*)(W + (int64_t)(32 * ft0 + r) * ldw + 8 * h);
@@ -116,14 +119,14 @@ __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int ldw, i
     for (int k = 0; k < kD; ++k) wf[k] = wp[2 * k];
     // activation fragments double-buffered one k-step ahead
     const bf16* ap = A + r * kLda + 8 * h;
-    bf16x8 bq[2][4];
+    bf16x8 bq[2][MT];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) bq[0][mt] = *reinterpret_cast<const bf16x8*>(ap + 32 * mt * kLda);
+    for (int mt = 0; mt < MT; ++mt) bq[0][mt] = *reinterpret_cast<const bf16x8*>(ap + 32 * mt * kLda);
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
         if (k + 1 < KS) {
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
+            for (int mt = 0; mt < MT; ++mt)
                 bq[(k + 1) & 1][mt] = *reinterpret_cast<const bf16x8*>(ap + 32 * mt * kLda + 16 * (k + 1));
         }
         const bf16x8 a = wf[k % kD];
@@ -135,16 +138,16 @@ __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int ldw, i
         // otherwise sink every load next to its use and expose its full latency)
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc[0][mt] = mfma32(a, bq[k & 1][mt], acc[0][mt]);
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma32(a, bq[k & 1][mt], acc[mt]);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 // tanh(acc + bias) -> bf16 row-major activation tile (4 consecutive features per 8-byte store)
 // (bk: the lane's 16 pre-scaled biases tanh_bias(b[32 ft + 8 g + 4 h + u]) at [4 g + u], or null)
-__device__ __forceinline__ void store_hidden(const f32x16 (&acc)[1][4], int ft, const float* bk, bf16* H, int lane) {
+template <int MT>
+__device__ __forceinline__ void store_hidden(const f32x16 (&acc)[MT], int ft, const float* bk, bf16* H, int lane) {
     const int r = lane & 31, h = lane >> 5;
-    constexpr int j = 0;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int f0 = 32 * ft + 8 * g + 4 * h;
@@ -154,11 +157,11 @@ __device__ __forceinline__ void store_hidden(const f32x16 (&acc)[1][4], int ft, 
                 for (int u = 0; u < 4; ++u) b[u] = bk[4 * g + u];
             }
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
+            for (int mt = 0; mt < MT; ++mt) {
                 bf16x4 v;
 #pragma unroll
                 for (int u = 0; u < 4; u += 2) {
-                    const f32x2 t = tanh_pre2(f32x2{acc[j][mt][4 * g + u], acc[j][mt][4 * g + u + 1]},
+                    const f32x2 t = tanh_pre2(f32x2{acc[mt][4 * g + u], acc[mt][4 * g + u + 1]},
                                               f32x2{b[u], b[u + 1]});
                     v[u] = to_bf16(t.x);
                     v[u + 1] = to_bf16(t.y);
@@ -169,20 +172,20 @@ __device__ __forceinline__ void store_hidden(const f32x16 (&acc)[1][4], int ft, 
 }
 
 // Y[m][f] <- bf16(acc[f][m] * (1 - Y[m][f]^2)) for this wave's features (tanh' gate, in place)
-__device__ __forceinline__ void gate_in_place(const f32x16 (&acc)[1][4], int ft, bf16* Y, int lane) {
+template <int MT>
+__device__ __forceinline__ void gate_in_place(const f32x16 (&acc)[MT], int ft, bf16* Y, int lane) {
     const int r = lane & 31, h = lane >> 5;
-    constexpr int j = 0;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int f0 = 32 * ft + 8 * g + 4 * h;
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
+            for (int mt = 0; mt < MT; ++mt) {
                 bf16x4* yp = reinterpret_cast<bf16x4*>(Y + (32 * mt + r) * kHp + f0);
                 const bf16x4 y = *yp;
                 bf16x4 v;
 #pragma unroll
                 for (int u = 0; u < 4; u += 2) {
-                    const f32x2 t = tanh_gate2(f32x2{acc[j][mt][4 * g + u], acc[j][mt][4 * g + u + 1]},
+                    const f32x2 t = tanh_gate2(f32x2{acc[mt][4 * g + u], acc[mt][4 * g + u + 1]},
                                                f32x2{from_bf16(y[u]), from_bf16(y[u + 1])});
                     v[u] = to_bf16(t.x);
                     v[u + 1] = to_bf16(t.y);
@@ -194,7 +197,7 @@ __device__ __forceinline__ void gate_in_place(const f32x16 (&acc)[1][4], int ft,
 
 // A [kTR][kH] bf16 tile of LDS (pitch kHp) -> rows m0.. of an HBM matrix (leading dimension ld),
 // nthr threads from thread index t0 (16-byte chunks, rows past `rows` skipped)
-template <int kThreads>
+template <int kThreads, int kTR>
 __device__ __forceinline__ void copy_tile_out_n(const bf16* T, bf16* out, int64_t ld, int64_t m0, int64_t rows,
                                                 int t, int diag) {
     constexpr int kChunks = kTR * (kH / 8);
@@ -222,12 +225,16 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 // kFW waves per workgroup: 4 (one per SIMD, 512 registers each) or 8 (two per SIMD)
 // kTrain: forward + heads + backward; otherwise the forward-only critic-value pass, which keeps
 // no launch-long accumulators and so fits two waves per SIMD.
-template <int kFW, bool kTrain>
-__global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
+template <int kFW, int kTR, bool kTrain>
+__global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedArgs p) {
+    using L = TileLds<kTR>;
+    constexpr int kOffX = L::kOffX, kOffH1 = L::kOffH1, kOffH2 = L::kOffH2, kOffD = L::kOffD;
+    constexpr int kHW = kTR / 32;  // waves running the heads (one 32-sample tile each)
+    constexpr int kMT = kTR / 32;  // 32-sample MFMA tiles of a tile
     constexpr int kFThreads = 64 * kFW;
     constexpr int kNT = kH / 32 / kFW;  // 32-wide feature tiles per wave
     static_assert(kHW <= kFW, "one 32-sample head tile per wave");
-    __shared__ __attribute__((aligned(16))) bf16 lds[kLdsElems];
+    __shared__ __attribute__((aligned(16))) bf16 lds[L::kElems];
     bf16* X = lds + kOffX;
     bf16* H1 = lds + kOffH1;
     bf16* H2 = lds + kOffH2;
@@ -315,8 +322,8 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
         // ---- L1, L2 (wave w: hidden features 64w .. 64w + 63, all 128 samples)
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
-            f32x16 acc[1][4];
-            fwd_tiles<kIn / 16, kXp, 1>(W1, kIn, ft0 + j, X, acc, lane);  // bias = W1 column 45 (X column 45 = 1)
+            f32x16 acc[kMT];
+            fwd_tiles<kIn / 16, kXp, kMT>(W1, kIn, ft0 + j, X, acc, lane);  // bias = W1 column 45 (X column 45 = 1)
             store_hidden(acc, ft0 + j, nullptr, H1, lane);
         }
         STAMP(2);
@@ -348,9 +355,9 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
         };
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
-            f32x16 acc[1][4];
+            f32x16 acc[kMT];
             bft = ft0 + j;
-            fwd_tiles<kH / 16, kHp, 1>(W2, kHx, ft0 + j, H1, acc, lane, [&]() {
+            fwd_tiles<kH / 16, kHp, kMT>(W2, kHx, ft0 + j, H1, acc, lane, [&]() {
                 if (j == kNT - 1) head_inputs();
                 else {
 #pragma unroll
@@ -369,7 +376,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
         // stores then retire while the head runs instead of holding the head's load waits
         if constexpr (kTrain && kFW > kHW) {
             if (wave >= kHW && p.h1_out)
-                copy_tile_out_n<64 * (kFW - kHW)>(H1, p.h1_out, kHx, m0, p.rows, tid - 64 * kHW, p.diag);
+                copy_tile_out_n<64 * (kFW - kHW), kTR>(H1, p.h1_out, kHx, m0, p.rows, tid - 64 * kHW, p.diag);
         }
         if (wave < kHW) {
             f32x16 acc;
@@ -488,7 +495,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
             continue;
         }
         if constexpr (kFW == kHW) {
-            if (p.h1_out) copy_tile_out_n<kFThreads>(H1, p.h1_out, kHx, m0, p.rows, tid, p.diag);
+            if (p.h1_out) copy_tile_out_n<kFThreads, kTR>(H1, p.h1_out, kHx, m0, p.rows, tid, p.diag);
         }
         STAMP(7);
         __syncthreads();
@@ -507,9 +514,9 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
         }
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
-            f32x16 acc[1][4];
+            f32x16 acc[kMT];
             // dH2^T = W3^T dout^T over head rows 0..15 (dout rows 16..31 are zero)
-            fwd_tiles<1, kDp, 1>(W3T, kOut, ft0 + j, D, acc, lane);
+            fwd_tiles<1, kDp, kMT>(W3T, kOut, ft0 + j, D, acc, lane);
             gate_in_place(acc, ft0 + j, H2, lane);
         }
         STAMP(9);
@@ -535,8 +542,8 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
         }
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
-            f32x16 acc[1][4];
-            fwd_tiles<kH / 16, kHp, 1>(W2T, kH, ft0 + j, H2, acc, lane);  // dH1^T = W2^T dH2^T
+            f32x16 acc[kMT];
+            fwd_tiles<kH / 16, kHp, kMT>(W2T, kH, ft0 + j, H2, acc, lane);  // dH1^T = W2^T dH2^T
             gate_in_place(acc, ft0 + j, H1, lane);                             // H1 is in HBM already
         }
         STAMP(11);
@@ -547,7 +554,7 @@ __global__ __launch_bounds__(64 * kFW, 1) void k_pg_fused(FusedArgs p) {
         //      so the next tile's X loads go out now
         if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
         // dH2 tile -> HBM (Y of the dW2 GEMM; H2 holds dH2 until the next tile's L2)
-        copy_tile_out_n<kFThreads>(H2, p.dh2_out, kH, m0, p.rows, tid, p.diag);
+        copy_tile_out_n<kFThreads, kTR>(H2, p.dh2_out, kH, m0, p.rows, tid, p.diag);
         if (tid < kH) {  // db2 stage 2: the kFW row-group sums of column tid, in row order
             const float* cs = reinterpret_cast<const float*>(lds + kOffD);
 #pragma unroll
@@ -666,7 +673,7 @@ extern "C" {
 
 int dxrl_pg_fused_sizes(int32_t* tile_rows, int64_t* partial_floats_per_block) {
     DXRL_REQUIRE(tile_rows && partial_floats_per_block, "null outputs");
-    *tile_rows = kTR;
+    *tile_rows = 128;  // the largest tile; launches use up to two workgroups per CU (grid <= 2 CUs)
     *partial_floats_per_block = kPartSize;
     return DXRL_OK;
 }
@@ -721,29 +728,51 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     f.dh2_out = static_cast<bf16*>(a->dh2);
     f.part = a->partial;
     f.loss = a->loss_partial;
-    const int64_t ntiles = (a->rows + kTR - 1) / kTR;
-    const int grid = (int)(ntiles < a->grid ? ntiles : a->grid);
+    // tile geometry: 128-sample tiles, one 8-wave workgroup per CU (160 KiB LDS), or 64-sample
+    // tiles, two 4-wave workgroups per CU (80 KiB each) -- DXRL_FUSED_TILE=64|128 (A/B)
+    static const int tile = [] {
+        const char* v = getenv("DXRL_FUSED_TILE");
+        return v && atoi(v) == 64 ? 64 : 128;
+    }();
+    static const int waves128 = [] {
+        const char* v = getenv("DXRL_FUSED_WAVES");  // A/B for 128-sample tiles: 4 = one wave per SIMD
+        return v && atoi(v) == 4 ? 4 : 8;
+    }();
+    static const int cus = [device] {
+        int n = 0;
+        return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0 ? n
+                                                                                                            : 256;
+    }();
+    const int waves = tile == 64 ? 4 : waves128;
+    const int64_t ntiles = (a->rows + tile - 1) / tile;
+    const int64_t cap = (int64_t)cus * (tile == 64 ? 2 : 1);
+    int64_t g64 = a->grid < cap ? a->grid : cap;
+    if (ntiles < g64) g64 = ntiles;
+    const int grid = (int)g64;
     static const int diag = [] {
         const char* v = getenv("DXRL_FUSED_DIAG");
         return v ? atoi(v) : 0;
     }();
     f.diag = diag;
-    static const int waves = [] {
-        const char* v = getenv("DXRL_FUSED_WAVES");  // A/B: 4 = one wave per SIMD
-        return v && atoi(v) == 4 ? 4 : 8;
-    }();
     static unsigned long long* stamps = nullptr;
     if ((diag & 8) && !stamps) (void)hipMalloc(&stamps, (size_t)65536 * 8 * 16 * 8);
     f.stamps = stamps;
-    if (!train) hipLaunchKernelGGL((k_pg_fused<8, false>), dim3(grid), dim3(512), 0, st, f);
-    else if (waves == 8) hipLaunchKernelGGL((k_pg_fused<8, true>), dim3(grid), dim3(512), 0, st, f);
-    else hipLaunchKernelGGL((k_pg_fused<4, true>), dim3(grid), dim3(256), 0, st, f);
+    if (tile == 64) {
+        if (!train) hipLaunchKernelGGL((k_pg_fused<4, 64, false>), dim3(grid), dim3(256), 0, st, f);
+        else hipLaunchKernelGGL((k_pg_fused<4, 64, true>), dim3(grid), dim3(256), 0, st, f);
+    } else if (!train) {
+        hipLaunchKernelGGL((k_pg_fused<8, 128, false>), dim3(grid), dim3(512), 0, st, f);
+    } else if (waves == 8) {
+        hipLaunchKernelGGL((k_pg_fused<8, 128, true>), dim3(grid), dim3(512), 0, st, f);
+    } else {
+        hipLaunchKernelGGL((k_pg_fused<4, 128, true>), dim3(grid), dim3(256), 0, st, f);
+    }
     if (int rc = launch_check("k_pg_fused")) return rc;
     if (diag & 8) {  // print the mean cycles per segment per wave (diagnostic builds only)
         std::vector<unsigned long long> h((size_t)grid * waves * 16);
         (void)hipStreamSynchronize(st);
         (void)hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost);
-        fprintf(stderr, "fused net=%d train=%d waves=%d cycles/wave:", a->net, (int)train, waves);
+        fprintf(stderr, "fused net=%d train=%d tile=%d waves=%d cycles/wave:", a->net, (int)train, tile, waves);
         for (int k = 0; k < 16; ++k) {
             double sum = 0;
             for (size_t w = 0; w < (size_t)grid * waves; ++w) sum += (double)h[w * 16 + k];

@@ -142,7 +142,8 @@ class PGTrainer:
         self.gnorm2 = torch.zeros(1, dtype=torch.float64, device=d)
         tr_, pf_ = C.c_int32(), C.c_int64()
         N.call("dxrl_pg_fused_sizes", C.byref(tr_), C.byref(pf_))
-        self.fused_grid = int(torch.cuda.get_device_properties(d).multi_processor_count)
+        # up to two learner workgroups per CU (64-sample tiles); the library clamps to its geometry
+        self.fused_grid = 2 * int(torch.cuda.get_device_properties(d).multi_processor_count)
         self.fused_partial = z(self.fused_grid + 17, pf_.value)  # + reduction scratch and sum
         self.fused_loss = torch.zeros(self.fused_grid, 4, dtype=torch.float64, device=d)
         self.pack()

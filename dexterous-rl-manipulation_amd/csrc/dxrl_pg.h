@@ -48,7 +48,16 @@ constexpr int64_t kBfW2c = kBfW1c + kW1;
 constexpr int64_t kBfW3c = kBfW2c + kW2;
 constexpr int64_t kBfW2cT = kBfW3c + kW3;
 constexpr int64_t kBfW3cT = kBfW2cT + kW2T;
-constexpr int64_t kBf = kBfW3cT + kW3T;
+// MFMA-fragment-ordered copies for the fused learner's weight streams: a [N][K] matrix as
+// [N / 32][K / 16][64 lanes][8], lane l of (feature tile ft, k-step k) holding W[32 ft + (l & 31)]
+// [16 k + 8 (l >> 5) .. + 7] -- every fragment load is one contiguous 1 KiB wave read.
+constexpr int64_t kFrW1 = (int64_t)kH * kIn, kFrW2 = (int64_t)kH * kH, kFrW3 = (int64_t)kOut * kH;
+constexpr int64_t kFrW2T = (int64_t)kH * kH, kFrW3T = (int64_t)kH * kOut;
+constexpr int64_t kFrNet = kFrW1 + kFrW2 + kFrW3 + kFrW2T + kFrW3T;
+constexpr int64_t kFr = kBfW3cT + kW3T;  // actor block, then critic block
+constexpr int64_t kFrOffW1 = 0, kFrOffW2 = kFrW1, kFrOffW3 = kFrOffW2 + kFrW2, kFrOffW2T = kFrOffW3 + kFrW3,
+                  kFrOffW3T = kFrOffW2T + kFrW2T;
+constexpr int64_t kBf = kFr + 2 * kFrNet;
 
 }  // namespace pg
 }  // namespace dxrl

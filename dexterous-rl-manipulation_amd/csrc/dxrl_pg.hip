@@ -1091,6 +1091,36 @@ __global__ void k_pack_weights(const float* __restrict__ p, bf16* __restrict__ w
         w[kBfW3aT + k] = to_bf16(p[kOffW3a + o * kHx + i]);
         w[kBfW3cT + k] = to_bf16(p[kOffW3c + o * kHx + i]);
     }
+    // fragment-ordered copies (dxrl_pg.h): element k of a [N][K] matrix's fragment stream
+    const auto frag_rc = [](int64_t k, int K, int64_t& row, int64_t& col) {
+        const int e = (int)(k & 7), lane = (int)((k >> 3) & 63);
+        const int64_t fk = k >> 9, ks = K / 16, ft = fk / ks, kk = fk % ks;
+        row = 32 * ft + (lane & 31);
+        col = 16 * kk + 8 * (lane >> 5) + e;
+    };
+#pragma unroll
+    for (int net = 0; net < 2; ++net) {
+        const int64_t o1 = net ? kOffW1c : kOffW1a, o2 = net ? kOffW2c : kOffW2a, o3 = net ? kOffW3c : kOffW3a;
+        bf16* f = w + kFr + net * kFrNet;
+        int64_t row, col;
+        if (k < kFrW1) {
+            frag_rc(k, kIn, row, col);
+            f[kFrOffW1 + k] = to_bf16(p[o1 + row * kIn + col]);
+        }
+        if (k < kFrW2) {
+            frag_rc(k, kH, row, col);
+            f[kFrOffW2 + k] = to_bf16(p[o2 + row * kHx + col]);
+            f[kFrOffW2T + k] = to_bf16(p[o2 + col * kHx + row]);  // W2T[row][col] = W2[col][row]
+        }
+        if (k < kFrW3) {
+            frag_rc(k, kH, row, col);
+            f[kFrOffW3 + k] = to_bf16(p[o3 + row * kHx + col]);
+        }
+        if (k < kFrW3T) {
+            frag_rc(k, kOut, row, col);
+            f[kFrOffW3T + k] = to_bf16(p[o3 + col * kHx + row]);  // W3T[row][col] = W3[col][row]
+        }
+    }
 }
 
 static int reduce_to(const double* partial, int nb, double* out, int slot, hipStream_t st) {

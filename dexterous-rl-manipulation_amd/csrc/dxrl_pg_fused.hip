@@ -72,10 +72,11 @@ typedef __attribute__((address_space(1))) const float gf32;
 struct FusedArgs {
     int net;    // 0 actor, 1 critic
     int train;  // 0: forward only (critic values), 1: forward + heads + backward
-    int diag;   // timing ablations (DXRL_FUSED_DIAG): 1 no HBM copies, 4 no dW MFMAs, 8 stamps
+    int diag;   // timing ablations (DXRL_FUSED_DIAG): 1 no HBM copies, 4 no dW MFMAs, 8 stamps,
+                // 16 no L2 epilogue, 32 no L2 MFMAs
     int64_t rows;
     const bf16* X;  // [rows][64], column 45 = 1
-    const bf16 *W1, *W2, *W3, *W2T, *W3T;
+    const bf16 *W1, *W2, *W3, *W2T, *W3T;  // fragment-ordered streams (dxrl_pg.h kFr*)
     const float* b2;  // bias of hidden unit n: b2[n * kHx]
     const float* b3;  // bias of head row o:   b3[o * kHx]
     const float* logstd;
@@ -105,18 +106,19 @@ struct NoHook {
     __device__ void operator()() const {}
 };
 template <int KS, int kLda, int MT, typename Hook = NoHook>
-__device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int ldw, int ft0, const bf16* A,
-                                          f32x16 (&acc)[MT], int lane, Hook hook = Hook{}) {
+__device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int kst, int ft0, const bf16* A,
+                                          f32x16 (&acc)[MT], int lane, Hook hook = Hook{}, bool no_mfma = false) {
     const int r = lane & 31, h = lane >> 5;
     constexpr int kD = KS < 8 ? KS : 8;  // weight prefetch distance (k-steps)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) zero_acc(acc[mt]);
     // weights through the global address space (global_load: vmcnt only -- a flat load would
     // also hold every LDS wait), kD k-steps ahead
-    const gbf16x8* wp = (const gbf16x8*)(W + (int64_t)(32 * ft0 + r) * ldw + 8 * h);
+    // (W: fragment-ordered stream of a matrix with kst k-steps per feature tile, dxrl_pg.h)
+    const gbf16x8* wp = (const gbf16x8*)W + (int64_t)ft0 * kst * 64 + lane;
     bf16x8 wf[kD];
 #pragma unroll
-    for (int k = 0; k < kD; ++k) wf[k] = wp[2 * k];
+    for (int k = 0; k < kD; ++k) wf[k] = wp[64 * k];
     // activation fragments double-buffered one k-step ahead
     const bf16* ap = A + r * kLda + 8 * h;
     bf16x8 bq[2][MT];
@@ -130,7 +132,7 @@ __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int ldw, i
                 bq[(k + 1) & 1][mt] = *reinterpret_cast<const bf16x8*>(ap + 32 * mt * kLda + 16 * (k + 1));
         }
         const bf16x8 a = wf[k % kD];
-        if (k + kD < KS) wf[k % kD] = wp[2 * (k + kD)];
+        if (k + kD < KS) wf[k % kD] = wp[64 * (k + kD)];
         // loads the caller wants behind the last weight fragment (vmcnt retires in issue order:
         // issued earlier they would hold every weight wait of this call)
         if (k + kD == KS) hook();
@@ -138,7 +140,8 @@ __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int ldw, i
         // otherwise sink every load next to its use and expose its full latency)
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma32(a, bq[k & 1][mt], acc[mt]);
+        for (int mt = 0; mt < MT; ++mt)
+            if (!no_mfma) acc[mt] = mfma32(a, bq[k & 1][mt], acc[mt]);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[kMT];
-            fwd_tiles<kIn / 16, kXp, kMT>(W1, kIn, ft0 + j, X, acc, lane);  // bias = W1 column 45 (X column 45 = 1)
+            fwd_tiles<kIn / 16, kXp, kMT>(W1, kIn / 16, ft0 + j, X, acc, lane);  // bias = W1 column 45 (X column 45 = 1)
             store_hidden(acc, ft0 + j, nullptr, H1, lane);
         }
         STAMP(2);
@@ -357,15 +360,15 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[kMT];
             bft = ft0 + j;
-            fwd_tiles<kH / 16, kHp, kMT>(W2, kHx, ft0 + j, H1, acc, lane, [&]() {
+            fwd_tiles<kH / 16, kHp, kMT>(W2, kH / 16, ft0 + j, H1, acc, lane, [&]() {
                 if (j == kNT - 1) head_inputs();
                 else {
 #pragma unroll
                     for (int q = 0; q < 16; ++q)
                         bk[q] = tanh_bias(((gf32*)b2)[(int64_t)(32 * bft + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
                 }
-            });
-            store_hidden(acc, ft0 + j, bk, H2, lane);
+            }, (p.diag & 32) != 0);
+            if (!(p.diag & 16)) store_hidden(acc, ft0 + j, bk, H2, lane);
         }
         STAMP(4);
         __syncthreads();
@@ -382,11 +385,11 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             f32x16 acc;
             zero_acc(acc);
             // W3 fragments in two batches of 8 (32 registers in flight)
-            const gbf16x8* wrow = (const gbf16x8*)(W3 + (int64_t)r * kHx + 8 * h);
+            const gbf16x8* wrow = (const gbf16x8*)W3 + lane;  // fragment stream, feature tile 0
             constexpr int kB = kH / 32;  // fragments per batch (two batches: 32 registers in flight)
             bf16x8 w3f[kB];
 #pragma unroll
-            for (int k = 0; k < kB; ++k) w3f[k] = wrow[2 * k];
+            for (int k = 0; k < kB; ++k) w3f[k] = wrow[64 * k];
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int k = 0; k < kB; ++k) {
@@ -395,7 +398,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int k = 0; k < kB; ++k) w3f[k] = wrow[2 * (k + kB)];
+            for (int k = 0; k < kB; ++k) w3f[k] = wrow[64 * (k + kB)];
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int k = 0; k < kB; ++k) {
@@ -516,7 +519,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[kMT];
             // dH2^T = W3^T dout^T over head rows 0..15 (dout rows 16..31 are zero)
-            fwd_tiles<1, kDp, kMT>(W3T, kOut, ft0 + j, D, acc, lane);
+            fwd_tiles<1, kDp, kMT>(W3T, kOut / 16, ft0 + j, D, acc, lane);
             gate_in_place(acc, ft0 + j, H2, lane);
         }
         STAMP(9);
@@ -543,7 +546,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[kMT];
-            fwd_tiles<kH / 16, kHp, kMT>(W2T, kH, ft0 + j, H2, acc, lane);  // dH1^T = W2^T dH2^T
+            fwd_tiles<kH / 16, kHp, kMT>(W2T, kH / 16, ft0 + j, H2, acc, lane);  // dH1^T = W2^T dH2^T
             gate_in_place(acc, ft0 + j, H1, lane);                             // H1 is in HBM already
         }
         STAMP(11);
@@ -704,11 +707,12 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     f.train = train;
     f.rows = a->rows;
     f.X = static_cast<const bf16*>(a->obs);
-    f.W1 = w + (c ? kBfW1c : kBfW1a);
-    f.W2 = w + (c ? kBfW2c : kBfW2a);
-    f.W3 = w + (c ? kBfW3c : kBfW3a);
-    f.W2T = w + (c ? kBfW2cT : kBfW2aT);
-    f.W3T = w + (c ? kBfW3cT : kBfW3aT);
+    const bf16* fr = w + kFr + (c ? kFrNet : 0);
+    f.W1 = fr + kFrOffW1;
+    f.W2 = fr + kFrOffW2;
+    f.W3 = fr + kFrOffW3;
+    f.W2T = fr + kFrOffW2T;
+    f.W3T = fr + kFrOffW3T;
     f.b2 = a->params + o2 + kH;
     f.b3 = a->params + o3 + kH;
     f.logstd = a->params + kOffLogStd;
@@ -791,8 +795,8 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     if (int rc = launch_check("k_fused_scatter")) return rc;
     // dW2[:, 0..255] = dH2^T H1 (the bias column 256 came from the column sums above)
     if (recompute)
-        return launch_wgrad_l1(static_cast<const bf16*>(a->dh2), kH, f.X, kIn, f.W1, a->rows, a->wgrad_splits,
-                               a->wgrad_partial, G + o2, st, kHx);
+        return launch_wgrad_l1(static_cast<const bf16*>(a->dh2), kH, f.X, kIn, w + (c ? kBfW1c : kBfW1a), a->rows,
+                               a->wgrad_splits, a->wgrad_partial, G + o2, st, kHx);
     return launch_wgrad(static_cast<const bf16*>(a->dh2), kH, kH, static_cast<const bf16*>(a->h1), kHx, kH, a->rows,
                         a->wgrad_splits, a->wgrad_partial, G + o2, st, kHx);
 }

@@ -48,7 +48,9 @@ BF["W2c"] = BF["W1c"] + W1
 BF["W3c"] = BF["W2c"] + W2
 BF["W2cT"] = BF["W3c"] + W3
 BF["W3cT"] = BF["W2cT"] + W2T
-NBF = BF["W3cT"] + W3T
+NBF_ROWS = BF["W3cT"] + W3T  # row-layout copies (GEMM chain, rollout)
+# + fragment-ordered streams of W1, W2, W3, W2T, W3T per network (fused learner; dxrl_pg.h kFr*)
+NBF = NBF_ROWS + 2 * (H * IN + H * H + OUT * H + H * H + H * OUT)
 LOGICAL_PARAMS = 2 * (OBS_IN * H + H) + 2 * (H * H + H) + (H * ACT + ACT) + (H + 1) + ACT  # 159,263
 
 

@@ -99,26 +99,33 @@ __device__ __forceinline__ void zero_acc(f32x16& a) {
     for (int q = 0; q < 16; ++q) a[q] = 0.0f;
 }
 
-// acc[mt] (features 32 ft0.. x samples 32 mt..) = W[32 ft0 + r][:] . A[32 mt + r][:]
-// over KS k-steps.  Weight fragments stream from L2 one 4-k-step chunk ahead (double
-// buffer); each weight fragment feeds MT MFMAs.
 struct NoHook {
     __device__ void operator()() const {}
 };
+// The first kD weight fragments of a fwd_tiles call, issuable ahead of the call (before the
+// barrier in front of its phase, so their L2 latency overlaps the barrier wait).
+template <int KS>
+struct WPre {
+    static constexpr int kD = KS < 8 ? KS : 8;  // weight prefetch distance (k-steps)
+    bf16x8 wf[kD];
+    const gbf16x8* wp;
+};
+// (W: fragment-ordered stream of a matrix with kst k-steps per feature tile, dxrl_pg.h; loads
+// through the global address space -- global_load: vmcnt only, a flat load would also hold every
+// LDS wait)
+template <int KS>
+__device__ __forceinline__ void w_prefetch(WPre<KS>& w, const bf16* W, int kst, int ft0, int lane) {
+    w.wp = (const gbf16x8*)W + (int64_t)ft0 * kst * 64 + lane;
+#pragma unroll
+    for (int k = 0; k < WPre<KS>::kD; ++k) w.wf[k] = w.wp[64 * k];
+}
 template <int KS, int kLda, int MT, typename Hook = NoHook>
-__device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int kst, int ft0, const bf16* A,
-                                          f32x16 (&acc)[MT], int lane, Hook hook = Hook{}, bool no_mfma = false) {
+__device__ __forceinline__ void fwd_run(WPre<KS>& w, const bf16* A, f32x16 (&acc)[MT], int lane, Hook hook = Hook{},
+                                        bool no_mfma = false) {
     const int r = lane & 31, h = lane >> 5;
-    constexpr int kD = KS < 8 ? KS : 8;  // weight prefetch distance (k-steps)
+    constexpr int kD = WPre<KS>::kD;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) zero_acc(acc[mt]);
-    // weights through the global address space (global_load: vmcnt only -- a flat load would
-    // also hold every LDS wait), kD k-steps ahead
-    // (W: fragment-ordered stream of a matrix with kst k-steps per feature tile, dxrl_pg.h)
-    const gbf16x8* wp = (const gbf16x8*)W + (int64_t)ft0 * kst * 64 + lane;
-    bf16x8 wf[kD];
-#pragma unroll
-    for (int k = 0; k < kD; ++k) wf[k] = wp[64 * k];
     // activation fragments double-buffered one k-step ahead
     const bf16* ap = A + r * kLda + 8 * h;
     bf16x8 bq[2][MT];
@@ -131,8 +138,8 @@ __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int kst, i
             for (int mt = 0; mt < MT; ++mt)
                 bq[(k + 1) & 1][mt] = *reinterpret_cast<const bf16x8*>(ap + 32 * mt * kLda + 16 * (k + 1));
         }
-        const bf16x8 a = wf[k % kD];
-        if (k + kD < KS) wf[k % kD] = wp[64 * (k + kD)];
+        const bf16x8 a = w.wf[k % kD];
+        if (k + kD < KS) w.wf[k % kD] = w.wp[64 * (k + kD)];
         // loads the caller wants behind the last weight fragment (vmcnt retires in issue order:
         // issued earlier they would hold every weight wait of this call)
         if (k + kD == KS) hook();
@@ -144,6 +151,15 @@ __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int kst, i
             if (!no_mfma) acc[mt] = mfma32(a, bq[k & 1][mt], acc[mt]);
         __builtin_amdgcn_sched_barrier(0);
     }
+}
+// acc[mt] (features 32 ft0.. x samples 32 mt..) = W[32 ft0 + r][:] . A[32 mt + r][:] over KS
+// k-steps; weight fragments stream from L2 kD k-steps ahead, each feeds MT MFMAs.
+template <int KS, int kLda, int MT, typename Hook = NoHook>
+__device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int kst, int ft0, const bf16* A,
+                                          f32x16 (&acc)[MT], int lane, Hook hook = Hook{}, bool no_mfma = false) {
+    WPre<KS> w;
+    w_prefetch(w, W, kst, ft0, lane);
+    fwd_run<KS, kLda, MT>(w, A, acc, lane, hook, no_mfma);
 }
 
 // tanh(acc + bias) -> bf16 row-major activation tile (4 consecutive features per 8-byte store)
@@ -329,6 +345,9 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             fwd_tiles<kIn / 16, kXp, kMT>(W1, kIn / 16, ft0 + j, X, acc, lane);  // bias = W1 column 45 (X column 45 = 1)
             store_hidden(acc, ft0 + j, nullptr, H1, lane);
         }
+        // the first W2 fragments go out before the barrier (their L2 latency overlaps its wait)
+        WPre<kH / 16> pw2;
+        w_prefetch(pw2, W2, kH / 16, ft0, lane);
         STAMP(2);
         __syncthreads();
         STAMP(3);
@@ -360,14 +379,16 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[kMT];
             bft = ft0 + j;
-            fwd_tiles<kH / 16, kHp, kMT>(W2, kH / 16, ft0 + j, H1, acc, lane, [&]() {
+            const auto l2_hook = [&]() {
                 if (j == kNT - 1) head_inputs();
                 else {
 #pragma unroll
                     for (int q = 0; q < 16; ++q)
                         bk[q] = tanh_bias(((gf32*)b2)[(int64_t)(32 * bft + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
                 }
-            }, (p.diag & 32) != 0);
+            };
+            if (j == 0) fwd_run<kH / 16, kHp, kMT>(pw2, H1, acc, lane, l2_hook, (p.diag & 32) != 0);
+            else fwd_tiles<kH / 16, kHp, kMT>(W2, kH / 16, ft0 + j, H1, acc, lane, l2_hook, (p.diag & 32) != 0);
             if (!(p.diag & 16)) store_hidden(acc, ft0 + j, bk, H2, lane);
         }
         STAMP(4);
@@ -500,6 +521,8 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         if constexpr (kFW == kHW) {
             if (p.h1_out) copy_tile_out_n<kFThreads, kTR>(H1, p.h1_out, kHx, m0, p.rows, tid, p.diag);
         }
+        WPre<1> pw3t;  // dH2's one W3T fragment, ahead of the barrier
+        w_prefetch(pw3t, W3T, kOut / 16, ft0, lane);
         STAMP(7);
         __syncthreads();
         STAMP(8);
@@ -519,9 +542,12 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[kMT];
             // dH2^T = W3^T dout^T over head rows 0..15 (dout rows 16..31 are zero)
-            fwd_tiles<1, kDp, kMT>(W3T, kOut / 16, ft0 + j, D, acc, lane);
+            if (j == 0) fwd_run<1, kDp, kMT>(pw3t, D, acc, lane);
+            else fwd_tiles<1, kDp, kMT>(W3T, kOut / 16, ft0 + j, D, acc, lane);
             gate_in_place(acc, ft0 + j, H2, lane);
         }
+        WPre<kH / 16> pw2t;  // dH1's first W2T fragments, ahead of the barrier
+        w_prefetch(pw2t, W2T, kH / 16, ft0, lane);
         STAMP(9);
         __syncthreads();
         STAMP(10);
@@ -546,7 +572,8 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[kMT];
-            fwd_tiles<kH / 16, kHp, kMT>(W2T, kH / 16, ft0 + j, H2, acc, lane);  // dH1^T = W2^T dH2^T
+            if (j == 0) fwd_run<kH / 16, kHp, kMT>(pw2t, H2, acc, lane);  // dH1^T = W2^T dH2^T
+            else fwd_tiles<kH / 16, kHp, kMT>(W2T, kH / 16, ft0 + j, H2, acc, lane);
             gate_in_place(acc, ft0 + j, H1, lane);                             // H1 is in HBM already
         }
         STAMP(11);

@@ -6,7 +6,7 @@ from collections import OrderedDict
 rows = list(csv.DictReader(open(sys.argv[1])))
 agg = OrderedDict()
 for r in rows:
-    name = r["Kernel_Name"].split("(")[0][:60]
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:60]
     key = (name, r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"])
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
     a = agg.setdefault(key, [0, 0.0])

@@ -29,6 +29,9 @@ MAX_CURRICULA = 256
 SUCCESS_TRAINING = 0
 SUCCESS_TERMINATED = 1
 ABI_VERSION = 1
+EVAL_POLICY_SIMPLE = 0
+EVAL_POLICY_HEURISTIC = 1
+EVAL_POLICY_RANDOM = 2
 
 
 class Curriculum(C.Structure):
@@ -96,6 +99,22 @@ class PgFusedArgs(C.Structure):
                 ("grads", C.c_void_p), ("h1_mode", C.c_int32)]
 
 
+class EvalSegment(C.Structure):
+    _fields_ = [("curriculum_row", C.c_int32), ("num_episodes", C.c_int32), ("first_episode", C.c_int32),
+                ("reserved", C.c_int32), ("obs_noise_std", C.c_double), ("dyn_noise_std", C.c_double),
+                ("noise_offset", C.c_int64), ("noise_count", C.c_int64)]
+
+
+class EvalArgs(C.Structure):
+    _fields_ = [("num_lanes", C.c_int32), ("policy", C.c_int32), ("max_steps", C.c_int32),
+                ("total_episodes", C.c_int32), ("lane_segments", C.c_void_p), ("segments", C.c_void_p),
+                ("mean_action", C.c_void_p), ("exploration_noise", C.c_double), ("policy_tape", C.c_void_p),
+                ("policy_stride", C.c_int64), ("noise_tape", C.c_void_p), ("reset_tape", C.c_void_p),
+                ("policy_seed", C.c_uint64), ("noise_seed", C.c_uint64), ("reset_seed", C.c_uint64)] + \
+               [(k, C.c_void_p) for k in ("ep_return", "ep_length", "ep_success", "ep_contacts", "contact_hist",
+                                          "policy_used", "status")]
+
+
 _P = C.c_void_p
 _I32, _I64, _F64 = C.c_int32, C.c_int64, C.c_double
 _SIGS = {
@@ -128,6 +147,7 @@ _SIGS = {
     "dxrl_pg_grad_sumsq": (C.c_int, [_I32, _P, _I64, _P, _P, _P]),
     "dxrl_pg_fused_sizes": (C.c_int, [C.POINTER(_I32), C.POINTER(_I64)]),
     "dxrl_pg_fused": (C.c_int, [_I32, C.POINTER(PgFusedArgs), _P]),
+    "dxrl_evaluate": (C.c_int, [_P, C.POINTER(EvalArgs), _P]),
     "dxrl_pg_adam": (C.c_int, [_I32, _P, _P, _P, _P, _I64, _F64, _F64, _F64, _F64, _I64, _P, _F64, _P]),
 }
 

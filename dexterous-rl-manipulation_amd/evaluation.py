@@ -10,6 +10,9 @@
   reference's order: dynamics noise before the step, observation noise
   after).  The vectorised trainer injects the same noise inside its fused
   rollout kernel instead.
+* ``Evaluator`` / ``RobustnessTester`` (evaluator.py) and ``EvaluationMetrics`` /
+  ``FailureType`` / ``format_metrics_report`` (metrics.py) are re-exported here
+  under the reference's module path (evaluation/__init__.py).
 """
 from __future__ import annotations
 
@@ -197,3 +200,14 @@ class CombinedNoiseWrapper(_NoiseBase):
     def step(self, action):
         obs, r, te, tr, info = self.env.step(self._act_noise(action, self.dynamics_noise_std))
         return self._obs_noise(obs, self.observation_noise_std), r, te, tr, info
+
+
+_LAZY = {"Evaluator": "evaluator", "RobustnessTester": "evaluator", "EvaluationMetrics": "metrics",
+         "FailureType": "metrics", "format_metrics_report": "metrics"}
+
+
+def __getattr__(name):
+    if name in _LAZY:
+        import importlib
+        return getattr(importlib.import_module(f".{_LAZY[name]}", __package__), name)
+    raise AttributeError(name)

@@ -335,6 +335,70 @@ typedef struct dxrl_pg_fused_args {
 int dxrl_pg_fused_sizes(int32_t* tile_rows, int64_t* partial_floats_per_block);
 int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* args, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Evaluation episode programs:
+ *   evaluation/evaluator.py:71-271      Evaluator.evaluate_episode / evaluate_heldout_set
+ *   evaluation/robustness_tests.py:240-407 RobustnessTester.evaluate_with_noise / run_robustness_sweep
+ * A LANE runs a chain of SEGMENTS back to back; a segment is one fresh env
+ * instance (DexterousManipulationEnv(curriculum_config=row), so its first reset
+ * draws the spawn position and later resets keep the object where it is,
+ * manipulation_env.py:156-161), optionally wrapped in CombinedNoiseWrapper(obs
+ * std, dyn std) (robustness_tests.py:140-211), running `num_episodes`
+ * consecutive reset(seed) -> loop{select_action, step} episodes, each stopping
+ * at terminated / truncated / max_steps with success = terminated
+ * (evaluator.py:150-158, robustness_tests.py:288-303).  The policy is frozen
+ * (evaluator.py:50-70: no update) and obs-independent, as every reference
+ * policy is; its random stream runs on across the lane's segments, the noise
+ * stream restarts with each segment's wrapper.
+ *
+ * Exact reference order = ONE lane whose segments are the driver's loop (the
+ * global np.random stream is consumed serially); the vectorised form = one lane
+ * per episode (or per noise level) with its own policy stream.
+ * ------------------------------------------------------------------------ */
+#define DXRL_EVAL_POLICY_SIMPLE 0    /* frozen SimpleLearner: clip(mean + f32(0 + s g), -1, 1)  (simple_learner.py:59-71) */
+#define DXRL_EVAL_POLICY_HEURISTIC 1 /* clip(-0.5f + f32(-0.1 + 0.2 u), -1, 1)         (heuristic_policy.py:38-63) */
+#define DXRL_EVAL_POLICY_RANDOM 2    /* Box.sample(): f32(-1 + 2 u)                     (random_policy.py:29-40)    */
+
+typedef struct dxrl_eval_segment {
+    int32_t curriculum_row;   /* row of the env's curriculum table                          */
+    int32_t num_episodes;     /* consecutive episodes on this instance                      */
+    int32_t first_episode;    /* record index of its first episode                           */
+    int32_t reserved;
+    double obs_noise_std;     /* wrapper observation noise (0 = off; consumes 45 normals per draw) */
+    double dyn_noise_std;     /* wrapper dynamics noise (0 = off; 15 normals per step)       */
+    int64_t noise_offset;     /* tape mode: first standard normal of this wrapper's stream    */
+    int64_t noise_count;      /* tape mode: normals available from noise_offset               */
+} dxrl_eval_segment;
+
+typedef struct dxrl_eval_args {
+    int32_t num_lanes;               /* <= env num_envs; lane i uses env slot i's weights    */
+    int32_t policy;                  /* DXRL_EVAL_POLICY_*                                    */
+    int32_t max_steps;               /* episode loop bound (evaluator.py:136)                */
+    int32_t total_episodes;          /* record count (bounds check)                          */
+    const int32_t* lane_segments;    /* device i32 [num_lanes + 1] CSR offsets into segments */
+    const dxrl_eval_segment* segments; /* device                                            */
+    const float* mean_action;        /* device f32 [num_lanes][15] (SIMPLE; NULL -> zeros)   */
+    double exploration_noise;        /* SIMPLE sigma (simple_learner.py:28)                  */
+    /* parity tapes (NULL -> device Philox streams) */
+    const double* policy_tape;       /* f64 [num_lanes][policy_stride] raw draws: legacy gauss
+                                        (SIMPLE) / next_double (HEURISTIC, RANDOM)           */
+    int64_t policy_stride;
+    const double* noise_tape;        /* f64 standard normals, addressed by segment offsets   */
+    const double* reset_tape;        /* f64 [total_episodes][D+6] resolved reset draws       */
+    uint64_t policy_seed, noise_seed, reset_seed; /* Philox keys of the device streams       */
+    /* per-episode records [total_episodes] */
+    double* ep_return;               /* episode_reward (f64, sequential sum)                 */
+    int32_t* ep_length;              /* episode_steps                                        */
+    uint8_t* ep_success;             /* terminated at the last step                          */
+    uint8_t* ep_contacts;            /* num_contacts of the last step's info                 */
+    uint8_t* contact_hist;           /* u8 [total_episodes][max_steps] per-step num_contacts
+                                        (contact_history, evaluator.py:148-150; nullable)   */
+    int32_t* policy_used;            /* i32 [num_lanes] policy draws consumed (nullable)     */
+    int32_t* status;                 /* i32 [1] device error word: 1 = a tape ran out        */
+} dxrl_eval_args;
+
+int dxrl_evaluate(dxrl_env* env, const dxrl_eval_args* args, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

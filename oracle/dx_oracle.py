@@ -276,3 +276,66 @@ def oracle_noisy_action(action, noise):
 def oracle_noisy_obs(obs, noise):
     """evaluation/robustness_tests.py:199-207: obs + f32(n) (f32 add)."""
     return (obs + np.asarray(noise).astype(np.float32)).astype(np.float32)
+
+
+# ---------------------------------------------------------------- evaluation episode programs
+POLICY_SIMPLE, POLICY_HEURISTIC, POLICY_RANDOM = 0, 1, 2
+
+
+def oracle_policy_action(kind: int, mean, sigma: float, draws):
+    """One frozen-policy action from 15 raw draws:
+    SimpleLearner  clip(mean + f32(0 + s g), -1, 1)           (simple_learner.py:59-71)
+    Heuristic      clip(f32(-0.5) + f32(-0.1 + 0.2 u), -1, 1)   (heuristic_policy.py:51-63)
+    Random         f32(-1 + 2 u)  (Box.sample: uniform(low, high).astype(f32))"""
+    if kind == POLICY_SIMPLE:
+        return [_clip(f32(m + f32(0.0 + sigma * g)), f32(-1), f32(1)) for m, g in zip(mean, draws)]
+    if kind == POLICY_HEURISTIC:
+        return [_clip(f32(f32(-0.5) + f32(-0.1 + (0.1 - -0.1) * u)), f32(-1), f32(1)) for u in draws]
+    return [f32(-1.0 + (1.0 - -1.0) * u) for u in draws]
+
+
+def oracle_eval_program(curricula, lane_off, segments, reset_tape, policy_tapes, noise_tape, kind: int, mean,
+                        sigma: float, max_steps: int, dense: bool = True, max_episode_steps: int = 200):
+    """Restates the evaluation drivers' episode loops (evaluation/evaluator.py:71-181 per
+    episode on a fresh env; robustness_tests.py:240-310 consecutive episodes on one
+    env inside CombinedNoiseWrapper) for a lane/segment plan (include/dxrl.h
+    dxrl_eval_segment fields as a structured array).  Returns per-episode
+    (return, length, success, final contacts, per-step contact counts)."""
+    E = int(sum(int(s["num_episodes"]) for s in segments))
+    ret = np.zeros(E)
+    length = np.zeros(E, np.int32)
+    succ = np.zeros(E, bool)
+    cont = np.zeros(E, np.int32)
+    hist = [None] * E
+    for lane in range(len(lane_off) - 1):
+        pcur = 0
+        ptape = policy_tapes[lane]
+        for si in range(lane_off[lane], lane_off[lane + 1]):
+            sg = segments[si]
+            env = OracleEnv(cur=curricula[int(sg["curriculum_row"])], dense=dense,
+                            max_episode_steps=max_episode_steps)
+            o_on, d_on = sg["obs_noise_std"] > 0.0, sg["dyn_noise_std"] > 0.0
+            ncur = int(sg["noise_offset"])
+            for ep in range(int(sg["num_episodes"])):
+                rec = int(sg["first_episode"]) + ep
+                env.reset(reset_tape[rec])
+                if o_on:
+                    ncur += 45  # wrapper reset: obs noise (values unused by obs-independent policies)
+                total, te, h = 0.0, False, []
+                for step in range(max_steps):
+                    a = oracle_policy_action(kind, mean[lane] if mean is not None else None, sigma,
+                                             ptape[pcur:pcur + D])
+                    pcur += D
+                    if d_on:
+                        g = noise_tape[ncur:ncur + D]
+                        ncur += D
+                        a = oracle_noisy_action(a, [0.0 + float(sg["dyn_noise_std"]) * x for x in g])
+                    _, r, te, tr = env.step(a)
+                    if o_on:
+                        ncur += 45
+                    total += r
+                    h.append(env.num_contacts)
+                    if te or tr:
+                        break
+                ret[rec], length[rec], succ[rec], cont[rec], hist[rec] = total, len(h), te, h[-1], h
+    return ret, length, succ, cont, hist

@@ -188,6 +188,50 @@ def test_large_batch_vs_oracle(pkg):
     assert np.all(env.step_count.cpu().numpy() == T)
 
 
+def test_streaming_step_policy_is_bit_identical(pkg, monkeypatch):
+    """N >= 2^19 steps stream with non-temporal loads/stores (dxrl_env.hip kNtMinEnvs); the
+    results are the default-policy kernel's bit for bit, and sampled lanes match the oracle."""
+    n, T = (1 << 19) + 37, 4
+    dev = torch.device("cuda:0")
+    envs = []
+    for v in ("0", "3"):
+        e = pkg.envs.VecEnv(n, curriculum_config=pkg.experiments.CurriculumConfig.variable(), reward_type="dense",
+                            seed=77, device=dev)
+        e.reset(write_obs=False)
+        envs.append((v, e))
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    outs = {}
+    for t in range(T):
+        a = (torch.rand(n, 15, generator=g, device=dev) * 2.6 - 1.3).contiguous()
+        for v, e in envs:
+            monkeypatch.setenv("DXRL_STEP_VARIANT", v)
+            outs[v] = [x.clone() for x in e.step(a)]
+        for x, y in zip(outs["0"], outs["3"]):
+            assert torch.equal(x, y)
+    monkeypatch.delenv("DXRL_STEP_VARIANT")
+    e = envs[1][1]
+    a = (torch.rand(n, 15, generator=g, device=dev) * 2.6 - 1.3).contiguous()
+    jp, jv = e.joint_positions.cpu().numpy(), e.joint_velocities.cpu().numpy()
+    op, ov = e.object_position.cpu().numpy(), e.object_velocity.cpu().numpy()
+    size, fric, mass = (x.cpu().numpy() for x in (e.object_size, e.friction_coefficient, e.object_mass))
+    flags, tcount = e.flags.cpu().numpy(), e.step_count.cpu().numpy()
+    ob, rw, te, tr = (x.cpu().numpy() for x in e.step(a))  # default policy at this N: streaming
+    an = a.cpu().numpy()
+    for i in [0, 1, 255, 256, 4097, n // 2, n - 1]:
+        o = OracleEnv(cur=OracleCurriculum(object_size=size[i], friction_coefficient=fric[i], object_mass=mass[i]))
+        o.jp, o.jv = [np.float32(x) for x in jp[:, i]], [np.float32(x) for x in jv[:, i]]
+        o.op, o.ov = [float(x) for x in op[:, i]], [np.float32(x) for x in ov[:, i]]
+        o.op_is_f32 = bool(flags[i] & (1 << 17))
+        o.contacts = [int((flags[i] >> f) & 1) for f in range(5)]
+        o.prev = [int((flags[i] >> (8 + f)) & 1) for f in range(5)] if flags[i] & (1 << 16) else None
+        o.t = int(tcount[i])
+        o.size, o.fric, o.mass = float(size[i]), float(fric[i]), float(mass[i])
+        eo, er, et, etr = o.step(an[i])
+        assert np.array_equal(ob[i], eo) and math.isclose(rw[i], er, rel_tol=REW_RTOL, abs_tol=1e-15)
+        assert (bool(te[i]), bool(tr[i])) == (et, etr)
+
+
 def test_device_rng_reset_ranges_and_sticky(pkg):
     n = 2048
     C = pkg.experiments.CurriculumConfig

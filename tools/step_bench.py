@@ -19,11 +19,23 @@ for _ in range(3):
     env.step(acts)
 torch.cuda.synchronize()
 L = 30
-ev = [torch.cuda.Event(enable_timing=True) for _ in range(L + 1)]
-ev[0].record()
-for k in range(L):
-    env.step(acts)
-    ev[k + 1].record()
-torch.cuda.synchronize()
-ms = sum(ev[k].elapsed_time(ev[k + 1]) for k in range(L)) / L
-print(f"variant={os.environ.get('DXRL_STEP_VARIANT', '0')} envs={n} ms={ms:.4f} GB/s={594 * n / (ms * 1e-3) / 1e9:.1f}")
+variants = os.environ.get("VARIANTS", "default").split(",")
+res = {v: [] for v in variants}
+for rep in range(int(os.environ.get("REPS", "1"))):
+    for v in variants:
+        if v == "default":
+            os.environ.pop("DXRL_STEP_VARIANT", None)
+        else:
+            os.environ["DXRL_STEP_VARIANT"] = v
+        env.step(acts)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(L + 1)]
+        ev[0].record()
+        for k in range(L):
+            env.step(acts)
+            ev[k + 1].record()
+        torch.cuda.synchronize()
+        res[v].append(sum(ev[k].elapsed_time(ev[k + 1]) for k in range(L)) / L)
+for v in variants:
+    ms = sorted(res[v])[len(res[v]) // 2]
+    print(f"variant={v} envs={n} median ms={ms:.4f} GB/s={594 * n / (ms * 1e-3) / 1e9:.1f} "
+          f"all={[round(x, 4) for x in res[v]]}")

@@ -112,7 +112,7 @@ class EvalArgs(C.Structure):
                 ("policy_stride", C.c_int64), ("noise_tape", C.c_void_p), ("reset_tape", C.c_void_p),
                 ("policy_seed", C.c_uint64), ("noise_seed", C.c_uint64), ("reset_seed", C.c_uint64)] + \
                [(k, C.c_void_p) for k in ("ep_return", "ep_length", "ep_success", "ep_contacts", "contact_hist",
-                                          "policy_used", "status")]
+                                          "policy_used", "status", "obs_traj", "act_traj")]
 
 
 _P = C.c_void_p

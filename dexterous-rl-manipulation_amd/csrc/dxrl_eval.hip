@@ -194,6 +194,9 @@ __global__ __launch_bounds__(64) void k_eval(const dxrl_curriculum* __restrict__
                 env_key(a.reset_seed, rec, rk0, rk1);
                 env_reset_philox(e, cu, rk0, rk1, 0);
             }
+            float* otraj = a.obs_traj ? a.obs_traj + rec * (int64_t)(a.max_steps + 1) * kObs : nullptr;
+            float* atraj = a.act_traj ? a.act_traj + rec * (int64_t)a.max_steps * kD : nullptr;
+            if (otraj) write_obs(e, otraj);
             double ret = 0.0;
             bool te = false, tr = false;
             uint32_t nc = 0;
@@ -210,6 +213,10 @@ __global__ __launch_bounds__(64) void k_eval(const dxrl_curriculum* __restrict__
                     act[k] = a.policy == DXRL_EVAL_POLICY_SIMPLE      ? clipf(mean[k] + nz[k], -1.0f, 1.0f)
                              : a.policy == DXRL_EVAL_POLICY_HEURISTIC ? clipf(-0.5f + nz[k], -1.0f, 1.0f)
                                                                       : nz[k];
+                if (atraj) {
+#pragma unroll
+                    for (int k = 0; k < kD; ++k) atraj[step * kD + k] = act[k];
+                }
                 if (dyn_noise) {  // RT:180-187: clip(a + f32(N(0, s)), low, high)
                     float dz[kD];
                     dyn_terms(ntape, sg.dyn_noise_std, ns, dz);
@@ -223,6 +230,7 @@ __global__ __launch_bounds__(64) void k_eval(const dxrl_curriculum* __restrict__
                 steps = step + 1;
                 nc = (uint32_t)__popc(e.flags & 0x1Fu);
                 if (hist) hist[step] = (uint8_t)nc;
+                if (otraj) write_obs(e, otraj + (int64_t)(step + 1) * kObs);
                 if (te || tr) break;
             }
             if (!ok) break;

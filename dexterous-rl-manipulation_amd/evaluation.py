@@ -203,7 +203,9 @@ class CombinedNoiseWrapper(_NoiseBase):
 
 
 _LAZY = {"Evaluator": "evaluator", "RobustnessTester": "evaluator", "EvaluationMetrics": "metrics",
-         "FailureType": "metrics", "format_metrics_report": "metrics"}
+         "FailureType": "metrics", "format_metrics_report": "metrics", "FailureMode": "failures",
+         "FailureModeDefinition": "failures", "FAILURE_MODE_DEFINITIONS": "failures", "FailureClassifier": "failures",
+         "FailureLogger": "failures", "EpisodeRecorder": "failures"}
 
 
 def __getattr__(name):

@@ -26,8 +26,9 @@ resolves random streams and assembles result dicts.  Two execution forms:
 
 The policies are the reference's three (all obs-independent): a frozen
 SimpleLearner (its ``mean_action`` + exploration noise), HeuristicPolicy and
-RandomPolicy; anything else raises TypeError.  ``failure_logger`` recording
-(evaluation/failure_logger.py) is not built yet and raises NotImplementedError.
+RandomPolicy; anything else raises TypeError.  With a ``failure_logger``
+(failures.FailureLogger) the kernel also records observation / action
+trajectories and every failed episode is logged as evaluator.py:101-179 does.
 """
 from __future__ import annotations
 
@@ -147,6 +148,8 @@ class EvalRecords:
     masses: np.ndarray
     frictions: np.ndarray
     policy_used: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    obs_traj: Optional[np.ndarray] = None  # f32 [E][max_steps + 1][45] (trajectories=True)
+    act_traj: Optional[np.ndarray] = None  # f32 [E][max_steps][15]
 
     def moments(self) -> HistoryMoments:
         return HistoryMoments.from_padded(self.contact_hist, self.ep_length)
@@ -241,7 +244,7 @@ class EpisodeProgram:
 
     def run(self, prog: _PolicyProgram, policy_tapes: Optional[np.ndarray] = None, host_resets: bool = True,
             host_noise: bool = True, device_seed: int = 0, keep_history: bool = True,
-            repeat: int = 1, timing: Optional[Dict] = None) -> EvalRecords:
+            repeat: int = 1, timing: Optional[Dict] = None, trajectories: bool = False) -> EvalRecords:
         """Launch the plan (``repeat`` back-to-back launches; ``timing['kernel_ms']`` =
         HIP-event time per launch on the launch stream)."""
         plan = self.plan(host_resets, host_noise)
@@ -266,6 +269,8 @@ class EpisodeProgram:
         out_con = torch.empty(E, dtype=torch.uint8, device=dev)
         out_hist = torch.zeros(E, ms, dtype=torch.uint8, device=dev) if keep_history else None
         used = torch.zeros(nl, dtype=torch.int32, device=dev)
+        o_traj = torch.zeros(E, ms + 1, OBS_DIM, dtype=torch.float32, device=dev) if trajectories else None
+        a_traj = torch.zeros(E, ms, ACTION_DIM, dtype=torch.float32, device=dev) if trajectories else None
         status = torch.zeros(1, dtype=torch.int32, device=dev)
         a = N.EvalArgs()
         a.num_lanes, a.policy, a.max_steps, a.total_episodes = nl, prog.kind, ms, E
@@ -278,6 +283,7 @@ class EpisodeProgram:
         a.ep_return, a.ep_length, a.ep_success = N.ptr(out_ret), N.ptr(out_len), N.ptr(out_suc)
         a.ep_contacts, a.contact_hist = N.ptr(out_con), N.ptr(out_hist)
         a.policy_used, a.status = N.ptr(used), N.ptr(status)
+        a.obs_traj, a.act_traj = N.ptr(o_traj), N.ptr(a_traj)
         with torch.cuda.device(dev):
             st = torch.cuda.current_stream(dev)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -295,7 +301,9 @@ class EpisodeProgram:
         return EvalRecords(out_ret.cpu().numpy(), out_len.cpu().numpy(), out_suc.cpu().numpy().astype(bool),
                            out_con.cpu().numpy(),
                            out_hist.cpu().numpy() if keep_history else np.zeros((E, 0), np.uint8),
-                           p[:, 0], p[:, 1], p[:, 2], used.cpu().numpy())
+                           p[:, 0], p[:, 1], p[:, 2], used.cpu().numpy(),
+                           o_traj.cpu().numpy() if trajectories else None,
+                           a_traj.cpu().numpy() if trajectories else None)
 
 
 _SEG_DTYPE = np.dtype([("curriculum_row", "<i4"), ("num_episodes", "<i4"), ("first_episode", "<i4"),
@@ -356,8 +364,6 @@ class Evaluator:
 
     def __init__(self, policy, heldout_set, reward_type: str = "dense", max_episode_steps: int = 200,
                  failure_logger=None, device=None):
-        if failure_logger is not None:
-            raise NotImplementedError("failure_logger trajectories (evaluation/failure_logger.py) are not built yet")
         self.policy = policy
         self.heldout_set = heldout_set
         self.reward_type = reward_type
@@ -395,9 +401,32 @@ class Evaluator:
         prog = policy_program(self.policy)
         p = self._program([eval_config])
         p.add_lane([Segment(0, [seed])])
-        rec = p.run(prog, policy_tapes=_exact_tape(prog, p))
+        rec = p.run(prog, policy_tapes=_exact_tape(prog, p), trajectories=self.failure_logger is not None)
         prog.stream.commit(int(rec.policy_used[0]))
-        return _episode_dicts(rec, np.arange(1), True)[0]
+        out = _episode_dicts(rec, np.arange(1), True)
+        self._log_failures(rec, out, [eval_config], [seed])
+        return out[0]
+
+    def _log_failures(self, rec: EvalRecords, episodes: List[Dict], configs, seeds):
+        """evaluator.py:101-179: EpisodeRecorder contents of each failed episode -> failure_logger."""
+        if self.failure_logger is None:
+            return
+        for i, ep in enumerate(episodes):
+            if ep["success"]:
+                continue
+            n = ep["episode_steps"]
+            cfg = configs[i]
+            cfg_dict = cfg.to_dict() if hasattr(cfg, "to_dict") else {
+                "object_size": cfg.object_size, "object_mass": cfg.object_mass,
+                "friction_coefficient": cfg.friction_coefficient}
+            states = [rec.obs_traj[i, k].copy() for k in range(n + 1)]
+            c0 = int(rec.obs_traj[i, 0, 40:45].sum())  # info["num_contacts"] after reset
+            contacts = [[1.0 if j < c0 else 0.0 for j in range(5)]] + ep["contact_history"]
+            meta = {"seed": seeds[i], "eval_config": cfg_dict, "object_size": ep["object_size"],
+                    "object_mass": ep["object_mass"], "friction_coefficient": ep["friction_coefficient"]}
+            self.failure_logger.log_episode(episode_data=ep, states=states,
+                                            actions=[rec.act_traj[i, k].copy() for k in range(n)],
+                                            contacts=contacts, metadata=meta, max_steps=self.max_episode_steps)
 
     def heldout_program(self, num_episodes_per_object: int, seed: Optional[int], parallel: bool) -> EpisodeProgram:
         """The launch plan of evaluate_heldout_set: object-major episodes (object i,
@@ -427,14 +456,20 @@ class Evaluator:
             self.freeze_policy()
         prog = policy_program(self.policy)
         p = self.heldout_program(num_episodes_per_object, seed, parallel)
+        traj = self.failure_logger is not None
         if not parallel:
-            rec = p.run(prog, policy_tapes=_exact_tape(prog, p))
+            rec = p.run(prog, policy_tapes=_exact_tape(prog, p), trajectories=traj)
             prog.stream.commit(int(rec.policy_used[0]))
         elif policy_seeds is not None:
-            rec = p.run(prog, policy_tapes=_seeded_tapes(prog, p, policy_seeds))
+            rec = p.run(prog, policy_tapes=_seeded_tapes(prog, p, policy_seeds), trajectories=traj)
         else:
-            rec = p.run(prog, host_resets=False, host_noise=False, device_seed=device_seed)
-        return self.results(rec, int(num_episodes_per_object), return_episodes)
+            rec = p.run(prog, host_resets=False, host_noise=False, device_seed=device_seed, trajectories=traj)
+        res = self.results(rec, int(num_episodes_per_object), return_episodes or traj)
+        if traj:
+            segs = [lane_seg for lane in p.lanes for lane_seg in lane]
+            self._log_failures(rec, res["all_episodes"], [p.configs[s.row] for s in segs],
+                               [s.episode_seeds[0] for s in segs])
+        return res
 
     def results(self, rec: EvalRecords, K: int, return_episodes: bool = True) -> Dict:
         """evaluator.py:229-262 result dicts from the episode records."""

@@ -309,6 +309,60 @@ class StepBasedScheduler(CurriculumScheduler):
 
 
 # ============================================================ ExperimentConfig tree
+class CurriculumLogger:
+    """experiments/curriculum_logger.py:13-130: per-episode curriculum state and the
+    scheduler's progression events, saved as JSON."""
+
+    def __init__(self, log_dir: str = "logs"):
+        from pathlib import Path
+        self.log_dir = Path(log_dir)
+        self.log_dir.mkdir(parents=True, exist_ok=True)
+        self.episode_logs: List[Dict] = []
+        self.progression_logs: List[Dict] = []
+
+    def log_episode(self, episode: int, scheduler: CurriculumScheduler, success: bool, episode_steps: int):
+        st = scheduler.get_statistics()
+        c = scheduler.current_config
+        self.episode_logs.append({
+            "episode": episode, "total_steps": scheduler.total_steps,
+            "difficulty_level": st["current_difficulty_level"], "success": success,
+            "episode_steps": episode_steps, "recent_success_rate": st["recent_success_rate"],
+            "object_size": c.object_size, "object_mass": c.object_mass,
+            "friction_coefficient": c.friction_coefficient})
+
+    def log_progression(self, scheduler: CurriculumScheduler, progression_occurred: bool):
+        if progression_occurred and scheduler.progression_history:
+            self.progression_logs.append(dict(scheduler.progression_history[-1]))
+
+    def save(self, filename: str = "curriculum_progression.json"):
+        path = self.log_dir / filename
+        with open(path, "w") as f:
+            json.dump({"episode_logs": self.episode_logs, "progression_logs": self.progression_logs}, f, indent=2)
+        return path
+
+    def print_progression_summary(self, scheduler: CurriculumScheduler):
+        st = scheduler.get_statistics()
+        bar = "=" * 60
+        lines = ["\n" + bar, "Curriculum Progression Summary", bar,
+                 f"Total episodes: {st['total_episodes']}", f"Total steps: {st['total_steps']}",
+                 f"Current difficulty level: {st['current_difficulty_level']:.2f}",
+                 f"Recent success rate: {st['recent_success_rate']:.3f}",
+                 f"Overall success rate: {st['overall_success_rate']:.3f}",
+                 f"Number of progressions: {st['num_progressions']}"]
+        if self.progression_logs:
+            lines += ["\nProgression History:", "-" * 60]
+            for k, p in enumerate(self.progression_logs, 1):
+                lines += [f"Progression {k}:", f"  Episode: {p.get('episode', 'N/A')}",
+                          f"  Total steps: {p.get('total_steps', 'N/A')}",
+                          f"  Difficulty level: {p.get('difficulty_level', 0):.2f}",
+                          f"  Success rate: {p.get('success_rate', 0):.3f}",
+                          f"  Object size: {p.get('object_size', 0):.4f} m",
+                          f"  Object mass: {p.get('object_mass', 0):.4f} kg",
+                          f"  Friction: {p.get('friction_coefficient', 0):.3f}", ""]
+        lines.append(bar)
+        print("\n".join(lines))
+
+
 class _Section:
     """to_dict / strict from_dict shared by the experiment sections."""
 

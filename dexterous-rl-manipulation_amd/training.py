@@ -212,3 +212,71 @@ def gather_records(count, cap, ret, length, success, end_step, gid0=0) -> Episod
     return EpisodeRecords(env_id=env_id[order], end_step=end[order], total_reward=ret.cpu().numpy()[m][order],
                           steps=length.cpu().numpy()[m][order],
                           success=success.cpu().numpy()[m][order].astype(bool), dropped=int((counts - kept).sum()))
+
+
+# ------------------------------------------------------------------ JSON training log
+class TrainingLogger:
+    """training/logger.py:12-133: per-episode reward / steps / success series, a
+    convergence episode (first reward above 0.5) and the JSON log format.
+    ``log_records`` appends a device rollout's EpisodeRecords in one call
+    (vectorised; the same series ``log_episode`` would build one by one)."""
+
+    def __init__(self, log_dir: str = "logs", experiment_name: str = "experiment"):
+        from pathlib import Path
+        self.log_dir = Path(log_dir)
+        self.experiment_name = experiment_name
+        self.log_dir.mkdir(parents=True, exist_ok=True)
+        self.convergence_threshold: float = 0.5
+        self.reset()
+
+    def reset(self):
+        self.episode_rewards: List[float] = []
+        self.episode_steps: List[int] = []
+        self.success_rates: List[float] = []
+        self.reward_components: List[Dict[str, float]] = []
+        self.convergence_step: Optional[int] = None
+
+    def log_episode(self, episode: int, reward: float, steps: int, success: bool,
+                    reward_components: Optional[Dict[str, float]] = None):
+        self.episode_rewards.append(reward)
+        self.episode_steps.append(steps)
+        self.success_rates.append(1.0 if success else 0.0)
+        if reward_components:
+            self.reward_components.append(dict(reward_components))
+        if self.convergence_step is None and reward > self.convergence_threshold:
+            self.convergence_step = episode
+
+    def log_records(self, records: "EpisodeRecords", first_episode: Optional[int] = None):
+        """Episodes of a rollout, in record order, numbered from ``first_episode``
+        (default: continuing this log)."""
+        base = len(self.episode_rewards) if first_episode is None else int(first_episode)
+        rew = np.asarray(records.total_reward, dtype=np.float64)
+        if self.convergence_step is None:
+            hit = np.flatnonzero(rew > self.convergence_threshold)
+            if len(hit):
+                self.convergence_step = base + int(hit[0])
+        self.episode_rewards += rew.tolist()
+        self.episode_steps += np.asarray(records.steps).astype(np.int64).tolist()
+        self.success_rates += np.where(np.asarray(records.success, dtype=bool), 1.0, 0.0).tolist()
+
+    def get_statistics(self, window_size: int = 10) -> Dict[str, float]:
+        if not self.episode_rewards:
+            return {}
+        r = self.episode_rewards
+        s = self.success_rates
+        rr, rs = r[-window_size:], s[-window_size:]
+        return {"total_episodes": len(r), "mean_reward": float(np.mean(r)), "std_reward": float(np.std(r)),
+                "recent_mean_reward": float(np.mean(rr)), "recent_std_reward": float(np.std(rr)),
+                "overall_success_rate": float(np.mean(s)), "recent_success_rate": float(np.mean(rs)),
+                "convergence_step": self.convergence_step,
+                "mean_episode_steps": float(np.mean(self.episode_steps)) if self.episode_steps else 0.0}
+
+    def save(self, filename: Optional[str] = None):
+        import json
+        path = self.log_dir / (filename or f"{self.experiment_name}_log.json")
+        data = {"experiment_name": self.experiment_name, "statistics": self.get_statistics(),
+                "episode_rewards": [float(x) for x in self.episode_rewards], "episode_steps": self.episode_steps,
+                "success_rates": [float(x) for x in self.success_rates], "reward_components": self.reward_components}
+        with open(path, "w") as f:
+            json.dump(data, f, indent=2)
+        return path

@@ -395,6 +395,12 @@ typedef struct dxrl_eval_args {
                                         (contact_history, evaluator.py:148-150; nullable)   */
     int32_t* policy_used;            /* i32 [num_lanes] policy draws consumed (nullable)     */
     int32_t* status;                 /* i32 [1] device error word: 1 = a tape ran out        */
+    /* trajectories (nullable; failure_logger.py:242-297 EpisodeRecorder, evaluator.py:101-152):
+       obs_traj f32 [total_episodes][max_steps + 1][45] -- the reset observation, then the
+       observation after every step; act_traj f32 [total_episodes][max_steps][15] -- the policy's
+       action of every step.  Rows past an episode's length are left untouched. */
+    float* obs_traj;
+    float* act_traj;
 } dxrl_eval_args;
 
 int dxrl_evaluate(dxrl_env* env, const dxrl_eval_args* args, void* stream);

@@ -39,6 +39,13 @@ from evaluation.robustness_tests import RobustnessTester  # noqa: E402
 from policies.heuristic_policy import HeuristicPolicy  # noqa: E402
 from policies.random_policy import RandomPolicy  # noqa: E402
 from policies.simple_learner import SimpleLearner  # noqa: E402
+from evaluation.failure_logger import FailureLogger  # noqa: E402
+from evaluation.failure_taxonomy import FailureClassifier  # noqa: E402
+from experiments.curriculum_logger import CurriculumLogger  # noqa: E402
+from experiments.curriculum_scheduler import CurriculumScheduler  # noqa: E402
+from experiments.config import CurriculumConfig  # noqa: E402
+from training.logger import TrainingLogger  # noqa: E402
+import tempfile  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
 
@@ -242,6 +249,71 @@ def metric_kats():
     return out
 
 
+def gen_failure_log():
+    """Evaluator + FailureLogger (evaluator.py:101-179): the logged entries minus timestamps."""
+    c = HELDOUT_CASES[0]
+    h = HeldOutObjectSet(G.make_cfg(c["heldout"][0]), num_heldout_objects=6, seed=c["heldout"][2])
+    pol = make_policy(c["policy"], MEANS[c["mean"]], None)
+    np.random.seed(c["np_seed"])
+    with tempfile.TemporaryDirectory() as d:
+        fl = FailureLogger(log_dir=d)
+        ev = Evaluator(pol, h, reward_type="dense", max_episode_steps=9, failure_logger=fl)
+        res = ev.evaluate_heldout_set(num_episodes_per_object=4, seed=c["seed"])
+        entries = [{k: v for k, v in e.items() if k != "timestamp"} for e in fl.logged_episodes]
+        stats = fl.get_statistics()
+    return dict(policy=c["policy"], mean=c["mean"], np_seed=c["np_seed"], heldout=[c["heldout"][0], 6, c["heldout"][2]],
+                K=4, seed=c["seed"], max_steps=9, entries=entries, statistics=stats,
+                steps=[r["episode_steps"] for r in res["all_episodes"]])
+
+
+def gen_taxonomy(metric_cases):
+    clf = FailureClassifier(success_threshold=3)
+    out = []
+    for case in metric_cases:
+        eps = [dict(e, contact_history=[[1.0 if i < c else 0.0 for i in range(5)] for c in e.get("contact_history", [])])
+               for e in case["episodes"]]
+        modes = [clf.classify(dict(e), case["max_steps"]) for e in eps]
+        try:
+            st = clf.get_failure_statistics([dict(e) for e in eps], case["max_steps"])
+            st.pop("classified_episodes")
+        except ZeroDivisionError:  # the reference divides by the episode count (failure_taxonomy.py:305)
+            st = "ZeroDivisionError"
+        out.append(dict(max_steps=case["max_steps"], episodes=case["episodes"],
+                        modes=[[m.value if m else None, conf] for m, conf in modes], statistics=st))
+    return out
+
+
+def gen_training_logs():
+    rng = np.random.default_rng(11)
+    with tempfile.TemporaryDirectory() as d:
+        tl = TrainingLogger(log_dir=d, experiment_name="kat")
+        rewards = rng.normal(0.2, 0.4, 57).tolist()
+        steps = rng.integers(1, 201, 57).tolist()
+        succ = (rng.random(57) < 0.4).tolist()
+        for k in range(57):
+            tl.log_episode(k, rewards[k], int(steps[k]), bool(succ[k]),
+                           reward_components={"distance": rewards[k] / 2} if k % 7 == 0 else None)
+        path = tl.save()
+        saved = json.load(open(path))
+        stats3 = tl.get_statistics(window_size=3)
+        sched = CurriculumScheduler(CurriculumConfig.easy(), CurriculumConfig.hard(), success_rate_threshold=0.3,
+                                    window_size=10, min_episodes_before_progression=10, progression_steps=3)
+        cl = CurriculumLogger(log_dir=d)
+        cs = (rng.random(80) < 0.6).tolist()
+        csteps = rng.integers(1, 201, 80).tolist()
+        for k in range(80):
+            prog = sched.update(bool(cs[k]), int(csteps[k]))
+            cl.log_episode(k, sched, bool(cs[k]), int(csteps[k]))
+            cl.log_progression(sched, prog)
+        cpath = cl.save()
+        csaved = json.load(open(cpath))
+        buf = io.StringIO()
+        with redirect_stdout(buf):
+            cl.print_progression_summary(sched)
+    return dict(rewards=rewards, steps=steps, success=succ, saved=saved, stats3=stats3,
+                curriculum_success=cs, curriculum_steps=csteps, curriculum_saved=csaved, summary=buf.getvalue())
+
+
 def main():
     meta = {"generator": "tests/golden/gen_eval_golden.py", "numpy": np.__version__,
             "means": MEANS,
@@ -249,6 +321,9 @@ def main():
             "per_episode": [gen_per_episode(c) for c in PER_EPISODE_CASES],
             "robustness": [gen_robust(c) for c in ROBUST_CASES],
             "metrics": metric_kats()}
+    meta["taxonomy"] = gen_taxonomy(meta["metrics"])
+    meta["failure_log"] = gen_failure_log()
+    meta["training_logs"] = gen_training_logs()
     with open(os.path.join(OUT, "eval_golden.json"), "w") as f:
         json.dump(jsonable(meta), f, indent=None, separators=(",", ":"))
     print("wrote", os.path.join(OUT, "eval_golden.json"))

@@ -183,3 +183,30 @@ def test_tape_overrun_and_bad_rows_raise():
     q.add_lane([evr.Segment(1, [1])])
     with pytest.raises(ValueError):
         q.run(prog, policy_tapes=np.zeros((1, 15 * 200)))
+
+
+def test_failure_logger_trajectories_match_reference(tmp_path):
+    """Evaluator(failure_logger=...) (evaluator.py:101-179): logged entries -- mode, confidence,
+    contact history incl. the reset row, metadata, obs / action trajectories -- as the reference logs them."""
+    from dexterous_rl_manipulation_amd import failures as F
+    g = golden()["failure_log"]
+    h = ev.HeldOutObjectSet(cfg_of(g["heldout"][0]), num_heldout_objects=g["heldout"][1], seed=g["heldout"][2])
+    pol = make_policy(g["policy"], golden()["means"][g["mean"]])
+    np.random.seed(g["np_seed"])
+    fl = F.FailureLogger(log_dir=str(tmp_path))
+    res = ev.Evaluator(pol, h, reward_type="dense", max_episode_steps=g["max_steps"],
+                       failure_logger=fl).evaluate_heldout_set(num_episodes_per_object=g["K"], seed=g["seed"])
+    assert [r["episode_steps"] for r in res["all_episodes"]] == g["steps"]
+    assert len(fl.logged_episodes) == len(g["entries"])
+    for got, want in zip(fl.logged_episodes, g["entries"]):
+        got = {k: v for k, v in got.items() if k != "timestamp"}
+        got["states"] = [list(map(float, s)) for s in got["states"]]
+        got["actions"] = [list(map(float, a)) for a in got["actions"]]
+        assert got.pop("episode_reward") == pytest.approx(want["episode_reward"], rel=1e-12)
+        want = {k: v for k, v in want.items() if k != "episode_reward"}
+        got["metadata"]["eval_config"] = {k: (list(v) if isinstance(v, tuple) else v)
+                                          for k, v in got["metadata"]["eval_config"].items()}
+        assert got == want
+    st = fl.get_statistics()
+    assert st["failure_mode_counts"] == g["statistics"]["failure_mode_counts"]
+    assert st["mean_reward"] == pytest.approx(g["statistics"]["mean_reward"], rel=1e-12)

@@ -69,7 +69,8 @@ class RolloutIO(C.Structure):
     _fields_ = [("gauss", C.c_void_p), ("gauss_stride", C.c_int64), ("reset_draws", C.c_void_p),
                 ("reset_stride", C.c_int64), ("record_cap", C.c_int32), ("ep_return", C.c_void_p),
                 ("ep_length", C.c_void_p), ("ep_success", C.c_void_p), ("ep_end_step", C.c_void_p),
-                ("ep_count", C.c_void_p), ("gauss_used", C.c_void_p), ("status", C.c_void_p)]
+                ("ep_count", C.c_void_p), ("gauss_used", C.c_void_p), ("status", C.c_void_p),
+                ("episode_budget", C.c_void_p)]
 
 
 class PgRolloutArgs(C.Structure):

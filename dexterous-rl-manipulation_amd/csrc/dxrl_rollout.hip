@@ -143,10 +143,11 @@ __global__ __launch_bounds__(64) void k_rollout_simple(EnvSoA s, LearnerSoA L, R
     const double* grow = kTape ? io.gauss + i * io.gauss_stride : nullptr;
     const double* rrow = kTape ? io.reset_draws + i * io.reset_stride : nullptr;
     int gcur = 0, done_eps = 0;
+    const int budget = io.episode_budget ? io.episode_budget[i] : 0x7fffffff;
     bool ok = true;
     const float fnoise = (float)p.noise, fclip = (float)p.clip;
 
-    for (int step = 0; step < p.num_steps; ++step) {
+    for (int step = 0; step < p.num_steps && done_eps < budget; ++step) {
         // select_action (SL:59-71)
         double g[kD];
         if (!draw_normals<kTape>(g, grow, io.gauss_stride, gcur, lk0, lk1, nctr)) {
@@ -184,6 +185,12 @@ __global__ __launch_bounds__(64) void k_rollout_simple(EnvSoA s, LearnerSoA L, R
                 if (io.ep_length) io.ep_length[o] = e.t;  // step + 1
                 if (io.ep_success) io.ep_success[o] = p.success_terminated ? (uint8_t)te : (uint8_t)0;
                 if (io.ep_end_step) io.ep_end_step[o] = step;
+            }
+            if (done_eps + 1 >= budget) {  // the driver's loop ends here: no further env.reset()
+                ++done_eps;
+                best = -__builtin_inf();
+                ep_ret = 0.0;
+                break;
             }
             // next run_episode: env.reset() (no seed) + policy.reset()
             const dxrl_curriculum cu = s.curricula[e.cfg];

@@ -164,8 +164,12 @@ class SimpleLearnerRollout:
         self.env.reset(draws=draws, write_obs=False)
         self.learner.reset()
 
-    def run(self, num_steps: int, collect: bool = True, env_index=None) -> Optional[EpisodeRecords]:
+    def run(self, num_steps: int, collect: bool = True, env_index=None,
+            episode_budget: Optional[torch.Tensor] = None) -> Optional[EpisodeRecords]:
+        """``num_steps`` steps of every env; ``episode_budget`` (i32 [N], device) stops an env
+        once it has finished that many episodes in this call."""
         io = N.RolloutIO()
+        io.episode_budget = N.ptr(episode_budget)
         io.record_cap = self.record_cap if collect else 0
         if collect:
             io.ep_return, io.ep_length = N.ptr(self.ep_return), N.ptr(self.ep_length)

@@ -178,6 +178,10 @@ typedef struct dxrl_rollout_io {
     int32_t* ep_count;        /* i32 [N] episodes finished in this call   */
     int32_t* gauss_used;      /* i32 [N] tape values consumed             */
     int32_t* status;          /* i32 [1] device error word (tape overrun) */
+    /* i32 [N] episode budget of this call (nullable = unbounded): an env stops once it has
+       finished that many episodes, before the next episode's env.reset() -- a driver's
+       `for episode in range(num_episodes)` loop (evaluation/component_ablation.py:154-166). */
+    const int32_t* episode_budget;
 } dxrl_rollout_io;
 
 int dxrl_learner_layout_for(int32_t num_envs, int32_t action_dim, dxrl_learner_layout* out);

@@ -314,6 +314,29 @@ def gen_training_logs():
                 curriculum_success=cs, curriculum_steps=csteps, curriculum_saved=csaved, summary=buf.getvalue())
 
 
+def gen_ablation():
+    """train_with_config (evaluation/component_ablation.py:78-195) for the four ablation
+    configurations x two seeds.  The reference seeds its env stream from OS entropy
+    (env.reset() without a seed); for capture the stand-in's lazy seeding is pinned to
+    env_seed, the value the build's train_with_config takes as its env_seed argument."""
+    from evaluation.component_ablation import AblationConfig as RAC, train_with_config as rtwc
+    from evaluation.component_ablation import compute_ablation_statistics as rstats
+    orig = G._pcg
+    runs, grouped = [], {}
+    try:
+        for name, cur, dense in [("baseline", True, True), ("no_curriculum", False, True),
+                                 ("no_dense_reward", True, False), ("minimal", False, False)]:
+            for seed, env_seed in [(42, 1001), (123, 1002)]:
+                G._pcg = lambda s, es=env_seed: orig(es if s is None else s)
+                r = rtwc(RAC(cur, dense, name), num_episodes=25, max_episode_steps=40, seed=seed)
+                runs.append(dict(name=name, use_curriculum=cur, use_dense_reward=dense, seed=seed, env_seed=env_seed,
+                                 result=r.to_dict(), np_random_after=np.random.standard_normal(2)))
+                grouped.setdefault(name, []).append(r)
+    finally:
+        G._pcg = orig
+    return dict(num_episodes=25, max_episode_steps=40, runs=runs, statistics=rstats(grouped))
+
+
 def main():
     meta = {"generator": "tests/golden/gen_eval_golden.py", "numpy": np.__version__,
             "means": MEANS,
@@ -324,6 +347,7 @@ def main():
     meta["taxonomy"] = gen_taxonomy(meta["metrics"])
     meta["failure_log"] = gen_failure_log()
     meta["training_logs"] = gen_training_logs()
+    meta["ablation"] = gen_ablation()
     with open(os.path.join(OUT, "eval_golden.json"), "w") as f:
         json.dump(jsonable(meta), f, indent=None, separators=(",", ":"))
     print("wrote", os.path.join(OUT, "eval_golden.json"))

@@ -87,3 +87,24 @@ def test_failure_logger_roundtrip(tmp_path):
     r.record_step(state=np.zeros(3), contacts=[1, 0])
     r.set_metadata(seed=1)
     assert r.get_recorded_data()["contacts"] == [[1.0, 0.0]]
+
+
+def test_ablation_config_and_statistics_match_reference():
+    """AblationConfig naming (reference tests/test_component_ablation.py:25-38) and
+    compute_ablation_statistics over the reference's own results."""
+    from dexterous_rl_manipulation_amd import ablation as A
+    assert A.AblationConfig(True, True).name == "curriculum_dense-reward"
+    assert A.AblationConfig(False, False).name == "no-curriculum_sparse-reward"
+    assert A.AblationConfig(True, False, name="custom").name == "custom"
+    g = golden()["ablation"]
+    grouped = {}
+    for r in g["runs"]:
+        d = r["result"]
+        cfg = A.AblationConfig(**d["config"])
+        grouped.setdefault(r["name"], []).append(A.TrainingResults(
+            cfg, d["episode_rewards"], d["episode_steps"], d["success_rates"], d["final_success_rate"],
+            d["mean_episode_length"], d["convergence_step"], d["total_episodes"]))
+        summ = A._summarise(cfg, np.array(d["episode_rewards"]), np.array(d["episode_steps"]),
+                            np.array(d["success_rates"]) > 0.5, d["total_episodes"])
+        assert summ.to_dict() == d
+    assert A.compute_ablation_statistics(grouped) == g["statistics"]

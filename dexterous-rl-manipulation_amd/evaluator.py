@@ -24,9 +24,11 @@ resolves random streams and assembles result dicts.  Two execution forms:
   draws (throughput form; distributionally equivalent, not the reference's
   numbers).
 
-The policies are the reference's three (all obs-independent): a frozen
-SimpleLearner (its ``mean_action`` + exploration noise), HeuristicPolicy and
-RandomPolicy; anything else raises TypeError.  With a ``failure_logger``
+The kernel compiles the reference's three policies (all obs-independent): a
+frozen SimpleLearner (its ``mean_action`` + exploration noise), HeuristicPolicy
+and RandomPolicy.  Any other object with ``select_action`` runs the same plan
+through the Gymnasium facade (device env steps, host policy calls, the
+reference's loop as written).  With a ``failure_logger``
 (failures.FailureLogger) the kernel also records observation / action
 trajectories and every failed episode is logged as evaluator.py:101-179 does.
 """
@@ -100,6 +102,14 @@ class _PolicyProgram:
     sigma: float
     stream: _HostStream
     seeded: Any  # seed -> fresh per-episode stream tape of n values
+
+
+def compiled_program(policy) -> Optional[_PolicyProgram]:
+    """policy_program, or None for a policy the kernel does not compile (host-policy path)."""
+    try:
+        return policy_program(policy)
+    except TypeError:
+        return None
 
 
 def policy_program(policy) -> _PolicyProgram:
@@ -306,6 +316,54 @@ class EpisodeProgram:
                            a_traj.cpu().numpy() if trajectories else None)
 
 
+    def run_facade(self, policy, trajectories: bool = False) -> EvalRecords:
+        """The plan's episodes in order through the Gymnasium facade (one device env step per
+        call) with a host policy -- the path for policies the kernel does not compile (any
+        ``select_action``), running evaluator.py:71-181 / robustness_tests.py:262-303 as
+        written: a fresh env per segment, CombinedNoiseWrapper when the segment is noisy."""
+        from .envs import DexterousManipulationEnv
+        from .evaluation import CombinedNoiseWrapper
+        E, ms = self.total_episodes, self.max_steps
+        ret, length = np.zeros(E), np.zeros(E, np.int32)
+        succ, cont = np.zeros(E, bool), np.zeros(E, np.uint8)
+        hist, props = np.zeros((E, ms), np.uint8), np.full((E, 3), np.nan)
+        otraj = np.zeros((E, ms + 1, OBS_DIM), np.float32) if trajectories else None
+        atraj = np.zeros((E, ms, ACTION_DIM), np.float32) if trajectories else None
+        k = 0
+        for seg in (s for lane in self.lanes for s in lane):
+            base = DexterousManipulationEnv(curriculum_config=self.configs[seg.row], reward_type=self.reward_type,
+                                            reward_shaping=self.reward_shaping,
+                                            max_episode_steps=self.max_episode_steps, device=self.device)
+            noisy = seg.obs_std > 0.0 or seg.dyn_std > 0.0
+            env = CombinedNoiseWrapper(base, seg.obs_std, seg.dyn_std, seed=seg.noise_seed) if noisy else base
+            for seed in seg.episode_seeds:
+                obs, info = env.reset(seed=seed)
+                if hasattr(policy, "reset"):
+                    policy.reset()
+                if trajectories:
+                    otraj[k, 0] = obs
+                total, te, n = 0.0, False, 0
+                for step in range(ms):
+                    a = policy.select_action(obs)
+                    if trajectories:
+                        atraj[k, step] = a
+                    obs, r, te, tr, info = env.step(a)
+                    total += r
+                    n = step + 1
+                    hist[k, step] = info.get("num_contacts", 0)
+                    if trajectories:
+                        otraj[k, step + 1] = obs
+                    if te or tr:
+                        break
+                ret[k], length[k], succ[k], cont[k] = total, n, bool(te), info.get("num_contacts", 0)
+                c = info["curriculum"]
+                props[k] = [c["object_size"], c["object_mass"], c["friction_coefficient"]]
+                k += 1
+            env.close()
+        return EvalRecords(ret, length, succ, cont, hist, props[:, 0], props[:, 1], props[:, 2],
+                           np.zeros(len(self.lanes), np.int32), otraj, atraj)
+
+
 _SEG_DTYPE = np.dtype([("curriculum_row", "<i4"), ("num_episodes", "<i4"), ("first_episode", "<i4"),
                        ("reserved", "<i4"), ("obs_noise_std", "<f8"), ("dyn_noise_std", "<f8"),
                        ("noise_offset", "<i8"), ("noise_count", "<i8")])
@@ -398,11 +456,15 @@ class Evaluator:
         """evaluator.py:71-181: one episode on a fresh env instance."""
         if not self._policy_frozen:
             self.freeze_policy()
-        prog = policy_program(self.policy)
+        prog = compiled_program(self.policy)
         p = self._program([eval_config])
         p.add_lane([Segment(0, [seed])])
-        rec = p.run(prog, policy_tapes=_exact_tape(prog, p), trajectories=self.failure_logger is not None)
-        prog.stream.commit(int(rec.policy_used[0]))
+        traj = self.failure_logger is not None
+        if prog is None:
+            rec = p.run_facade(self.policy, trajectories=traj)
+        else:
+            rec = p.run(prog, policy_tapes=_exact_tape(prog, p), trajectories=traj)
+            prog.stream.commit(int(rec.policy_used[0]))
         out = _episode_dicts(rec, np.arange(1), True)
         self._log_failures(rec, out, [eval_config], [seed])
         return out[0]
@@ -454,10 +516,12 @@ class Evaluator:
         """evaluator.py:183-262 (see heldout_program for the episode layout)."""
         if not self._policy_frozen:
             self.freeze_policy()
-        prog = policy_program(self.policy)
-        p = self.heldout_program(num_episodes_per_object, seed, parallel)
+        prog = compiled_program(self.policy)
+        p = self.heldout_program(num_episodes_per_object, seed, parallel and prog is not None)
         traj = self.failure_logger is not None
-        if not parallel:
+        if prog is None:  # host policy: the reference's sequential loop on the facade
+            rec = p.run_facade(self.policy, trajectories=traj)
+        elif not parallel:
             rec = p.run(prog, policy_tapes=_exact_tape(prog, p), trajectories=traj)
             prog.stream.commit(int(rec.policy_used[0]))
         elif policy_seeds is not None:
@@ -559,9 +623,11 @@ class RobustnessTester:
         return p
 
     def _run_levels(self, levels, num_episodes, seed, parallel, policy_seeds, device_seed):
-        prog = policy_program(self.policy)
-        p = self.levels_program(levels, num_episodes, seed, parallel)
-        if not parallel:
+        prog = compiled_program(self.policy)
+        p = self.levels_program(levels, num_episodes, seed, parallel and prog is not None)
+        if prog is None:  # host policy: the reference's sequential loop on the facade
+            rec = p.run_facade(self.policy)
+        elif not parallel:
             rec = p.run(prog, policy_tapes=_exact_tape(prog, p))
             prog.stream.commit(int(rec.policy_used[0]))
         elif policy_seeds is not None:

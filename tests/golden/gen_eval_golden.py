@@ -337,6 +337,36 @@ def gen_ablation():
     return dict(num_episodes=25, max_episode_steps=40, runs=runs, statistics=rstats(grouped))
 
 
+class ObsPolicy:
+    """A host policy the device kernel does not compile: deterministic, observation-dependent,
+    f32 actions; update() counts calls (Evaluator must freeze it, evaluator.py:50-61)."""
+
+    def __init__(self):
+        self.W = np.random.default_rng(5).normal(0, 0.5, (15, 45))
+        self.updates = 0
+
+    def select_action(self, obs):
+        return np.tanh(self.W @ np.asarray(obs, dtype=np.float64) + 0.3).astype(np.float32)
+
+    def update(self, reward):
+        self.updates += 1
+
+    def reset(self):
+        pass
+
+
+def gen_host_policy():
+    h = HeldOutObjectSet(G.make_cfg("easy"), num_heldout_objects=3, seed=123)
+    pol = ObsPolicy()
+    ev = Evaluator(pol, h, reward_type="dense", max_episode_steps=60)
+    res = ev.evaluate_heldout_set(num_episodes_per_object=2, seed=7)
+    rt = RobustnessTester(ObsPolicy(), G.make_cfg("variable"), reward_type="dense", max_episode_steps=50)
+    rob = rt.evaluate_with_noise(0.05, 0.05, num_episodes=3, seed=3)
+    return dict(episodes=[episode_record(r) for r in res["all_episodes"]], metrics=res["metrics"],
+                updates=pol.updates, robustness=[episode_record(e) for e in rob["episodes"]],
+                robustness_metrics=rob["metrics"])
+
+
 def main():
     meta = {"generator": "tests/golden/gen_eval_golden.py", "numpy": np.__version__,
             "means": MEANS,
@@ -348,6 +378,7 @@ def main():
     meta["failure_log"] = gen_failure_log()
     meta["training_logs"] = gen_training_logs()
     meta["ablation"] = gen_ablation()
+    meta["host_policy"] = gen_host_policy()
     with open(os.path.join(OUT, "eval_golden.json"), "w") as f:
         json.dump(jsonable(meta), f, indent=None, separators=(",", ":"))
     print("wrote", os.path.join(OUT, "eval_golden.json"))

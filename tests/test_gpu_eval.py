@@ -210,3 +210,41 @@ def test_failure_logger_trajectories_match_reference(tmp_path):
     st = fl.get_statistics()
     assert st["failure_mode_counts"] == g["statistics"]["failure_mode_counts"]
     assert st["mean_reward"] == pytest.approx(g["statistics"]["mean_reward"], rel=1e-12)
+
+
+class ObsPolicy:
+    """Same host policy as tests/golden/gen_eval_golden.py: observation-dependent, f32 actions."""
+
+    def __init__(self):
+        self.W = np.random.default_rng(5).normal(0, 0.5, (15, 45))
+        self.updates = 0
+
+    def select_action(self, obs):
+        return np.tanh(self.W @ np.asarray(obs, dtype=np.float64) + 0.3).astype(np.float32)
+
+    def update(self, reward):
+        self.updates += 1
+
+    def reset(self):
+        pass
+
+
+def test_host_policy_runs_through_facade():
+    """A policy the kernel does not compile (obs-dependent) runs the reference loop through the
+    facade: same episodes as the reference's Evaluator / RobustnessTester, policy frozen."""
+    g = golden()["host_policy"]
+    h = ev.HeldOutObjectSet(cfg_of("easy"), num_heldout_objects=3, seed=123)
+    pol = ObsPolicy()
+    e = ev.Evaluator(pol, h, reward_type="dense", max_episode_steps=60)
+    res = e.evaluate_heldout_set(num_episodes_per_object=2, seed=7, parallel=True)  # parallel ignored: host policy
+    for got, want in zip(res["all_episodes"], g["episodes"]):
+        check_episode(got, want)
+    close_dict(res["metrics"], g["metrics"])
+    assert pol.updates == g["updates"] == 0 and e._policy_frozen
+    e.unfreeze_policy()
+    assert not e._policy_frozen
+    rob = ev.RobustnessTester(ObsPolicy(), cfg_of("variable"), reward_type="dense",
+                              max_episode_steps=50).evaluate_with_noise(0.05, 0.05, num_episodes=3, seed=3)
+    for got, want in zip(rob["episodes"], g["robustness"]):
+        check_episode(got, want, with_props=False)
+    close_dict(rob["metrics"], g["robustness_metrics"])

@@ -21,6 +21,8 @@ promotion:
 * ``_sparse_reward``   <- rewards/reward_shaping.py:205-242
 * ``OracleSimpleLearner`` <- policies/simple_learner.py:49-99
 * ``oracle_run_episode``  <- training/episode_utils.py:13-55
+* ``oracle_eval_program`` <- evaluation/evaluator.py:71-181, robustness_tests.py:240-310
+  (pinned by tests/test_eval_host.py against tests/golden/eval_golden.json)
 """
 from __future__ import annotations
 

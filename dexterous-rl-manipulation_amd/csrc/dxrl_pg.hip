@@ -386,9 +386,9 @@ constexpr int kLsEnvs = 16;  // 16 lanes per env: envs per workgroup = 256 threa
 // standard normal k of Philox block k / 4 (Box-Muller pairs (x, y), (z, w)), as philox_normals
 __device__ __forceinline__ float philox_normal_at(int k, uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream) {
     const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)(k >> 2)}, k0, k1);
-    float n0, n1;
-    if ((k & 2) == 0) box_muller(r.x, r.y, n0, n1);
-    else box_muller(r.z, r.w, n0, n1);
+    float n0, n1;  // operands selected first: one branch-free Box-Muller (schedulable into MFMA gaps)
+    const bool hi = (k & 2) != 0;
+    box_muller(hi ? r.z : r.x, hi ? r.w : r.y, n0, n1);
     return (k & 1) ? n1 : n0;
 }
 
@@ -594,8 +594,25 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
         if (mlp) wave_layer<kIn / 16, kNT, true, 1>(X, kXs, w1frag, kCpw * wave, nullptr, 0, H1, kHs, lane);
         __syncthreads();
         LS_STAMP(1);
-        if (mlp) wave_layer<kH / 16, kNT, true, 1>(H1, kHs, w2frag, kCpw * wave, p.params + kOffW2a + kH, kHx, H2,
-                                                  kHs, lane);
+        // This step's Philox draws (action noise, dynamics noise, the next reset's two uniforms)
+        // depend only on counters, so they are issued in the L2 block, where the scheduler can
+        // place them in the gaps of the MFMA chain instead of on the step's serial path.
+        const int sa = s < kAct ? s : 0;
+        float eps = 0.0f, dzn = 0.0f;
+        double u1 = 0.0, u2 = 0.0;
+        const auto draws = [&]() {
+            eps = philox_normal_at(sa, pk0, pk1, ctr, kStreamPolicy);
+            if (p.dyn_noise > 0.0f) dzn = philox_normal_at(sa, pk0, pk1, ctr, kStreamDyn);
+            u1 = reset_uniform_at(s < kD ? s : 0, ek0, ek1, rctr);
+            u2 = reset_uniform_at(kD + s2, ek0, ek1, rctr);
+        };
+        if (mlp) {
+            draws();
+            wave_layer<kH / 16, kNT, true, 1>(H1, kHs, w2frag, kCpw * wave, p.params + kOffW2a + kH, kHx, H2, kHs,
+                                              lane);
+        } else {
+            draws();
+        }
         __syncthreads();
         LS_STAMP(2);
         if (mlp && wave == kRolloutWaves - 1) {  // mu head: 16 env rows x 32 head rows
@@ -615,9 +632,8 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
         LS_STAMP(3);
         if (!live) continue;
         // ---- a = mu + sigma * eps, log pi(a|s) in action order (gauss_logp's order)
-        const int sa = s < kAct ? s : 0;
         const float mu = mlp ? MU[eg * (kOut + 1) + sa] : 0.0f;
-        float a = mu + SIG[sa] * philox_normal_at(sa, pk0, pk1, ctr, kStreamPolicy);
+        float a = mu + SIG[sa] * eps;
         const float z = (a - mu) * ISIG[sa];
         const float term = -0.5f * z * z - LS[sa] - 0.5f * kLog2Pi;
         gx[kGxTerm + s] = term;
@@ -634,7 +650,7 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
         p.act[m * kActPad + s] = s < kAct ? a : 0.0f;
         if (s == 0) p.logp[m] = lp;
         if (p.dyn_noise > 0.0f)  // robustness_tests.py:180-187 (the tape keeps the policy's action)
-            a = clipf(a + p.dyn_noise * philox_normal_at(sa, pk0, pk1, ctr, kStreamDyn), -1.0f, 1.0f);
+            a = clipf(a + p.dyn_noise * dzn, -1.0f, 1.0f);
         LS_STAMP(4);
         bool te = false, tr = false;
         double r = 0.0;
@@ -717,8 +733,6 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
             sum_len += et;
             succ += te;
             // ---- env_reset_philox, lane-split: lane s draws slot s (joint) and slot 15 + s
-            const double u1 = reset_uniform_at(s < kD ? s : 0, ek0, ek1, rctr);
-            const double u2 = reset_uniform_at(kD + s2, ek0, ek1, rctr);
             const double v2 = has2 ? lo2 + (hi2 - lo2) * u2 : cst2;  // config.py:44-113 samplers
             if (s < kD) {
                 jp = (float)(-0.1 + (0.1 - -0.1) * u1);

@@ -393,3 +393,55 @@ def test_heldout_table_on_device(pkg):
     # a step on the held-out table advances without error and keeps the per-env objects
     env.step(torch.zeros(n, 15, device=env.device))
     assert np.array_equal(env.object_size.cpu().numpy(), size)
+
+
+def test_c4_full_size_heldout_vs_oracle(pkg):
+    """Config C4 at its full size: 8192 envs on the HeldOutObjectSet(hard, seed=42) table
+    (heldout_objects.py:46-143), device-RNG resets, 40 steps of random actions.  28 sampled
+    lanes (incl. the first, the tail and every 256-env workgroup boundary tested) re-simulated by
+    the CPU oracle from the device's own reset state; a second env with the same seed must
+    reproduce the whole batch bit-for-bit (the streams depend only on seed and env id)."""
+    n, T = 8192, 40
+    hs = pkg.evaluation.HeldOutObjectSet(pkg.experiments.CurriculumConfig.hard(), seed=42)
+    cfgs, idx = hs.native_table(n)
+    envs = []
+    for _ in range(2):
+        e = pkg.envs.VecEnv(n, reward_type="dense", seed=77)
+        e.set_curricula(cfgs, env_index=idx)
+        e.reset()
+        envs.append(e)
+    env, twin = envs
+    assert torch.equal(env.obs, twin.obs)
+    obs0 = env.obs.cpu().numpy()
+    jp, op = env.joint_positions.cpu().numpy(), env.object_position.cpu().numpy()
+    size, fric, mass = (t.cpu().numpy() for t in (env.object_size, env.friction_coefficient, env.object_mass))
+    rng = np.random.default_rng(8192)
+    lanes = np.unique(np.concatenate([[0, 255, 256, 4095, 4096, n - 1], rng.choice(n, 22, replace=False)]))
+    orcs = {}
+    for i in lanes:
+        o = hs.heldout_objects[i % len(hs.heldout_objects)]
+        assert (size[i], mass[i], fric[i]) == (o.size, o.mass, o.friction), i
+        orc = OracleEnv(cur=OracleCurriculum(object_size=size[i], friction_coefficient=fric[i],
+                                             object_mass=mass[i]), dense=True)
+        d = np.full(21, np.nan)
+        d[:15] = jp[:, i].astype(np.float64)
+        d[18:21] = op[:, i]
+        orc.reset(d)
+        assert np.array_equal(orc.obs(), obs0[i])
+        orcs[i] = orc
+    dev = env.device
+    for t in range(T):
+        a = torch.from_numpy(rng.uniform(-1.2, 1.2, size=(n, 15)).astype(np.float32)).to(dev)
+        ob, rw, te, tr = (x.cpu().numpy() for x in env.step(a))
+        tw = twin.step(a)
+        assert torch.equal(twin.obs, env.obs) and torch.equal(twin.reward, env.reward), t
+        an = a.cpu().numpy()
+        for i in lanes:
+            eo, er, et, etr = orcs[i].step(an[i])
+            assert np.array_equal(ob[i], eo), (t, i)
+            assert math.isclose(rw[i], er, rel_tol=REW_RTOL, abs_tol=1e-15), (t, i)
+            assert (bool(te[i]), bool(tr[i])) == (et, etr), (t, i)
+        assert np.array_equal(tw[2].cpu().numpy(), te)
+    assert np.all(np.abs(ob[:, :15]) <= 1.0)
+    assert np.array_equal(te.astype(bool), ob[:, 40:45].sum(1) >= 3)
+    assert np.all(env.step_count.cpu().numpy() == T)

@@ -14,10 +14,14 @@ GPU, MLP(256,256) learner, synthetic device-Philox randomness):
       (training/episode_utils.py:13-55, policies/simple_learner.py) for
       `horizon` steps per env, fused into one HIP launch.
 
-Multi-GPU (torchrun, one rank per GPU): env shards are independent (global env
-ids rank*N .. rank*N+N-1); the PG learner all-reduces one flat f32 gradient
-buffer per iteration; the timing uses a barrier + max-over-ranks.
-value = all ranks' env steps / max time (weak scaling).
+Multi-GPU, one rank per GPU over RCCL: either the driver's
+`torchrun --nproc-per-node N bench.py --gpus N`, or plain `bench.py --gpus N`,
+which starts that torchrun command as a child process before anything touches
+the GPU (and refuses when fewer than N GPUs are visible).  Env shards are
+independent (global env ids rank*N .. rank*N+N-1); the PG learner all-reduces
+the advantage moments and one flat f32 gradient buffer per iteration; the
+timing uses a barrier + max-over-ranks.  value = all ranks' env steps / max
+time (weak scaling).
 
 Also measured in-process (HIP events on the launch stream):
   * roofline: the standalone step kernel (dxrl_env_step, k_step) at a large N
@@ -43,15 +47,10 @@ STEP_BYTES_PER_ENV = 594  # k_step algorithmic bytes per env-step (DESIGN.md §4
 
 
 # BASELINE.json configs[1..4] as PG workloads (configs[0] is the CPU plumbing case)
-WORKLOADS = {
-    "easy": {"envs": 4096, "curriculum": "easy", "desc": "config_easy.json"},
-    "default": {"envs": 4096, "curriculum": "easy", "scheduler": True,
-                "desc": "config_default.json (CurriculumScheduler easy->hard fed by per-episode records)"},
-    "hard_heldout": {"envs": 8192, "curriculum": "hard", "heldout": True,
-                     "desc": "config_hard.json + HeldOutObjectSet table (env i -> object i % 10)"},
-    "variable_noise": {"envs": 4096, "curriculum": "variable", "obs_noise": 0.05, "dyn_noise": 0.05,
-                       "desc": "config_variable.json + fused obs/dynamics noise 0.05"},
-}
+_PKG = os.path.join(ROOT, "dexterous-rl-manipulation_amd")
+sys.path.insert(0, ROOT)
+import dexterous_rl_manipulation_amd  # noqa: E402,F401  (the package alias)
+from dexterous_rl_manipulation_amd.workloads import WORKLOADS, build_pg_workload  # noqa: E402
 
 
 def parse():
@@ -79,10 +78,33 @@ def parse():
     return a
 
 
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without torchrun: start N ranks (torch.distributed.run, one process
+    per GPU, rendezvous on 127.0.0.1) as a child process and return its exit code.  Called
+    before this process initialises the GPU (device_count() does not, on ROCm)."""
+    import socket
+    import subprocess
+    have = torch.cuda.device_count()
+    if have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {have}", file=sys.stderr)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -118,33 +140,12 @@ def pg_bench(args, world, rank, dev):
     """One bench step = one PGTrainer.iteration(): rollout (T env steps of every env, actor
     MLP fused) + critic forward + GAE + adv-norm + actor forward + heads + backward +
     RCCL gradient all-reduce (world > 1) + Adam."""
-    import dexterous_rl_manipulation_amd as pkg
-    from dexterous_rl_manipulation_amd import envs, trainer
-    n = args.envs
-    w = WORKLOADS[args.config]
-    env = envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.named(args.curriculum), reward_type="dense",
-                      seed=20240601, device=dev, global_env_offset=rank * n)
-    if w.get("heldout"):
-        from dexterous_rl_manipulation_amd import evaluation
-        ex = pkg.experiments.load_named_config("default")
-        hs = evaluation.HeldOutObjectSet(pkg.CurriculumConfig.named(args.curriculum),
-                                         num_heldout_objects=ex.evaluation.num_heldout_objects, seed=ex.evaluation.seed)
-        cfgs, idx = hs.native_table(n)
-        env.set_curricula(cfgs, env_index=(idx + rank * n) % len(cfgs))
     pg = None
     if world > 1:
         import torch.distributed as dist
         pg = dist.group.WORLD
-    tcfg = trainer.TrainerConfig(horizon=args.horizon, seed=7, obs_noise_std=w.get("obs_noise", 0.0),
-                                 dyn_noise_std=w.get("dyn_noise", 0.0), record_cap=16 if w.get("scheduler") else 0)
-    tr = trainer.PGTrainer(env, tcfg, process_group=pg, world_size=world)
-    if w.get("scheduler"):
-        sc = pkg.experiments.load_named_config("default").curriculum_scheduler
-        C = pkg.CurriculumConfig
-        tr.attach_curriculum(pkg.experiments.CurriculumScheduler(
-            C.named(sc.initial_difficulty), C.named(sc.target_difficulty), sc.success_rate_threshold,
-            sc.min_episodes_before_progression, sc.window_size, sc.progression_steps))
-    env.reset(write_obs=False)
+    env, tr = build_pg_workload(args.config, dev, rank=rank, world=world, process_group=pg, envs=args.envs,
+                                horizon=args.horizon, curriculum=args.curriculum)
     for _ in range(args.warmup):
         tr.iteration()
     torch.cuda.synchronize(dev)
@@ -160,8 +161,6 @@ def pg_bench(args, world, rank, dev):
     # phase breakdown (one extra iteration, outside the timed region)
     stream = torch.cuda.current_stream(dev)
     names = tr.phases()
-    if tr.scheduler is not None:
-        names.append("_feed_scheduler")  # records D2H + CurriculumScheduler.update_batch + table push
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
     evs[0].record(stream)
     for k, nm in enumerate(names):
@@ -171,7 +170,7 @@ def pg_bench(args, world, rank, dev):
     phases = {nm: round(evs[k].elapsed_time(evs[k + 1]), 4) for k, nm in enumerate(names)}
     M = tr.M
     gemm_ms = sum(v for k, v in phases.items() if k not in ("rollout", "advantages", "optimizer_step",
-                                                            "_feed_scheduler"))
+                                                            "schedule_feed", "schedule_apply"))
     train_flops = M * (FWD_BOTH + BWD_BOTH)
     mfma = {"bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_BF16_TFS,
             "training_gemms_achieved": round(train_flops / (gemm_ms * 1e-3) / 1e12, 2),
@@ -290,6 +289,8 @@ def cpu_baseline(args):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world, rank, local = dist_setup(args)
     dev = torch.device("cuda", local if world > 1 else 0)
     total_steps = args.envs * world * args.horizon * args.steps
@@ -300,7 +301,8 @@ def main():
                     f"{args.horizon} env steps x {args.envs} envs + critic fwd + GAE + adv-norm + PPO heads + "
                     f"backward + Adam")
         dtype = "bf16 MFMA (f32 acc) + f32/f64 env"
-        par = f"dp{world} (env shards, RCCL all-reduce of f32 grads)" if world > 1 else "dp1"
+        par = (f"dp{world} (env shards; RCCL all-reduce of the f64 advantage moments and the f32 grads)"
+               if world > 1 else "dp1")
         extra = {"phases_ms": phases, "mfma": mfma, "train_stats": stats}
     else:
         wall, kernel_ms = rollout_bench(args, world, rank, dev)
@@ -317,7 +319,8 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": dtype,
         "data": "synthetic (device Philox4x32-10 reset draws, policy / learner noise; random-init weights)",
         "config": {"workload": workload, "learner": args.learner, "envs_per_gpu": args.envs,
-                   "global_envs": args.envs * world, "horizon": args.horizon, "parallelism": par},
+                   "global_envs": args.envs * world, "horizon": args.horizon, "parallelism": par,
+                   "world_size": world, "backend": "nccl (RCCL over xGMI)" if world > 1 else None},
     }
     out.update(extra)
     if rank == 0 and not args.no_roofline:

@@ -80,7 +80,7 @@ class PgRolloutArgs(C.Structure):
                                           "ep_sum_return", "ep_sum_length", "ep_successes")] + \
                [("diag_flags", C.c_int32), ("success_rule", C.c_int32), ("record_cap", C.c_int32),
                 ("rec_return", C.c_void_p), ("rec_length", C.c_void_p), ("rec_success", C.c_void_p),
-                ("rec_end_step", C.c_void_p)]
+                ("rec_end_step", C.c_void_p), ("ep_code", C.c_void_p), ("applied_act", C.c_void_p)]
 
 
 class PgHeadsArgs(C.Structure):
@@ -98,6 +98,17 @@ class PgFusedArgs(C.Structure):
                [(k, C.c_void_p) for k in ("values", "h1", "dh2", "partial", "loss_partial")] + \
                [("grid", C.c_int32), ("wgrad_splits", C.c_int32), ("wgrad_partial", C.c_void_p),
                 ("grads", C.c_void_p), ("h1_mode", C.c_int32)]
+
+
+class SchedArgs(C.Structure):
+    _fields_ = [("codes", C.c_void_p), ("world", C.c_int32), ("horizon", C.c_int32), ("num_envs", C.c_int64),
+                ("window", C.c_int32), ("max_candidates", C.c_int32), ("threshold", C.c_double),
+                ("min_episodes", C.c_int64), ("episodes_before", C.c_int64)] + \
+               [(k, C.c_void_p) for k in ("tail_in", "tail_len_in", "tail_out", "tail_len_out", "scratch")] + \
+               [("scratch_bytes", C.c_int64), ("summary", C.c_void_p)]
+
+
+SCHED_MAX_CANDIDATES = 64  # DXRL_SCHED_MAX_CANDIDATES
 
 
 class EvalSegment(C.Structure):
@@ -144,11 +155,14 @@ _SIGS = {
     "dxrl_pg_rollout": (C.c_int, [_P, _P, _P, C.POINTER(PgRolloutArgs), _P]),
     "dxrl_pg_gae": (C.c_int, [_I32, _P, _P, _P, _I64, _I64, _F64, _F64, _P, _P, _P, _P, _P]),
     "dxrl_pg_adv_finalize": (C.c_int, [_I32, _I32, _P, _I64, _P, _P, _P]),
+    "dxrl_pg_adv_combine": (C.c_int, [_I32, _P, _I32, _P, _P]),
     "dxrl_pg_heads": (C.c_int, [_I32, C.POINTER(PgHeadsArgs), _P]),
     "dxrl_pg_grad_sumsq": (C.c_int, [_I32, _P, _I64, _P, _P, _P]),
     "dxrl_pg_fused_sizes": (C.c_int, [C.POINTER(_I32), C.POINTER(_I64)]),
     "dxrl_pg_fused": (C.c_int, [_I32, C.POINTER(PgFusedArgs), _P]),
     "dxrl_evaluate": (C.c_int, [_P, C.POINTER(EvalArgs), _P]),
+    "dxrl_sched_scratch_bytes": (C.c_int, [_I32, _I32, _I64, _I32, C.POINTER(_I64)]),
+    "dxrl_sched_scan": (C.c_int, [_I32, C.POINTER(SchedArgs), _P]),
     "dxrl_pg_adam": (C.c_int, [_I32, _P, _P, _P, _P, _I64, _F64, _F64, _F64, _F64, _I64, _P, _F64, _P]),
 }
 

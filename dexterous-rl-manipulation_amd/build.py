@@ -12,7 +12,7 @@ import subprocess
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
-SOURCES = ["dxrl_env.hip", "dxrl_rollout.hip", "dxrl_gemm.hip", "dxrl_pg.hip", "dxrl_pg_fused.hip", "dxrl_eval.hip"]
+SOURCES = ["dxrl_env.hip", "dxrl_rollout.hip", "dxrl_gemm.hip", "dxrl_pg.hip", "dxrl_pg_fused.hip", "dxrl_eval.hip", "dxrl_sched.hip"]
 HEADERS = ["dxrl_device.h", "dxrl_internal.h", "dxrl_mfma.h", "dxrl_gemm.h", "dxrl_pg.h"]
 OUT = os.path.join(PKG_DIR, "libdxrl.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

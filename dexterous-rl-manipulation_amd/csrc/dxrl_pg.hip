@@ -79,6 +79,8 @@ struct PgRolloutArgs {
     int32_t* rec_length;
     uint8_t* rec_success;
     int32_t* rec_end_step;
+    uint16_t* ep_code;   // [T N] scheduler feed: 0, or (episode length << 1) | success (nullable)
+    float* applied_act;  // [T N][kActPad] the action the env integrated (nullable; parity checks)
     unsigned long long* stamps;  // diag & 32 (k_pg_rollout_ls): cycles per step segment
 };
 
@@ -331,6 +333,10 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout(PgRolloutA
 #pragma unroll
                 for (int k = 0; k < kAct; ++k) a[k] = clipf(a[k] + p.dyn_noise * dn[k], -1.0f, 1.0f);
             }
+            if (p.applied_act) {
+#pragma unroll
+                for (int k = 0; k < kActPad; ++k) p.applied_act[m * kActPad + k] = k < kAct ? a[k] : 0.0f;
+            }
             bool te = false, tr = false;
             double cp[4], r = 0.0;
             if (!(p.diag & 2)) r = env_step(e, a, true, p.w, p.max_episode_steps, te, tr, cp);
@@ -338,6 +344,8 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout(PgRolloutA
             const bool d = !(p.diag & 2) && (te || tr || e.t >= p.max_steps);
             p.rew[m] = (float)r;
             p.done[m] = d;
+            if (p.ep_code)
+                p.ep_code[m] = d ? (uint16_t)((e.t << 1) | (p.success_terminated && te ? 1 : 0)) : (uint16_t)0;
             if (d) {
                 if (cnt < p.record_cap) {
                     const int64_t o = i * p.record_cap + cnt;
@@ -651,6 +659,7 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
         if (s == 0) p.logp[m] = lp;
         if (p.dyn_noise > 0.0f)  // robustness_tests.py:180-187 (the tape keeps the policy's action)
             a = clipf(a + p.dyn_noise * dzn, -1.0f, 1.0f);
+        if (p.applied_act) p.applied_act[m * kActPad + s] = s < kAct ? a : 0.0f;
         LS_STAMP(4);
         bool te = false, tr = false;
         double r = 0.0;
@@ -719,6 +728,8 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
         if (s == 0) {
             p.rew[m] = (float)r;
             p.done[m] = d;
+            if (p.ep_code)
+                p.ep_code[m] = d ? (uint16_t)((et << 1) | (p.success_terminated && te ? 1 : 0)) : (uint16_t)0;
         }
         if (d) {
             if (s == 0 && cnt < p.record_cap) {
@@ -801,17 +812,43 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
 // delta_t = r_t + gamma V_{t+1} (1 - d_t) - V_t ; A_t = delta_t + gamma lambda (1 - d_t) A_{t+1}
 // One thread per env scans t = T-1 .. 0 (coalesced across envs), 64-env workgroups so the scan
 // spreads over 64 CUs.  The loads of kGaeChunk steps go out together before that chunk's
-// recurrence runs (one HBM latency per chunk, not per step).  Block partials of sum A and
-// sum A^2 (f64) for the normalisation: partial[b] and partial[nb + b].
+// recurrence runs (one HBM latency per chunk, not per step).
+//
+// Normalisation moments without cancellation: each env accumulates f64 sums of (A - K) and
+// (A - K)^2 about its own first value K = A_{T-1}, giving (count, mean, M2) with M2 the sum of
+// squared deviations; workgroups, the block partials and the ranks then merge these triples
+// with Chan et al.'s pairwise update in a fixed order (deterministic).  A plain
+// sum(A^2) - mean sum(A) loses ~(mean/std)^2 ulps (2.8e-6 relative at mean/std = 4.6e4).
+struct Moments {
+    double n, mean, m2;
+};
+__device__ __forceinline__ Moments merge(Moments a, Moments b) {
+    const double n = a.n + b.n;
+    if (b.n == 0.0) return a;
+    if (a.n == 0.0) return b;
+    const double d = b.mean - a.mean;
+    return Moments{n, a.mean + d * (b.n / n), a.m2 + b.m2 + d * d * (a.n * b.n / n)};
+}
+// workgroup tree merge in LDS (fixed pairing), result in red[0]
+template <int NT>
+__device__ void block_merge(Moments v, Moments* red) {
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int w = NT / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] = merge(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+}
+
 constexpr int kGaeChunk = 32, kGaeThreads = 64;
 __global__ __launch_bounds__(kGaeThreads) void k_gae(const float* __restrict__ rew, const uint8_t* __restrict__ done,
                                                      const float* __restrict__ V, int64_t n, int64_t T, float gamma,
                                                      float lam, float* __restrict__ adv, float* __restrict__ ret,
-                                                     double* __restrict__ partial) {
-    __shared__ double red[2][kGaeThreads];
+                                                     Moments* __restrict__ partial) {
+    __shared__ Moments red[kGaeThreads];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t ic = i < n ? i : n - 1;  // clamped: every lane loads, only real envs store
-    double s = 0.0, s2 = 0.0;
+    double s = 0.0, s2 = 0.0, K = 0.0;
     float next_adv = 0.0f;
     float next_v = V[T * n + ic];
     for (int64_t hi = T; hi > 0; hi -= kGaeChunk) {
@@ -833,83 +870,51 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(const float* __restrict__ r
             const float delta = rv[k] + gamma * next_v * nd - vv[k];
             const float a = delta + gamma * lam * nd * next_adv;
             const int64_t m = (lo + k) * n + ic;
+            if (lo + k == T - 1) K = (double)a;
             if (i < n) {
                 adv[m] = a;
                 ret[m] = a + vv[k];
-                s += a;
-                s2 += (double)a * (double)a;
+                const double d = (double)a - K;
+                s += d;
+                s2 += d * d;
             }
             next_adv = a;
             next_v = vv[k];
         }
     }
-    red[0][threadIdx.x] = s;
-    red[1][threadIdx.x] = s2;
-    __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) {
-            red[0][threadIdx.x] += red[0][threadIdx.x + w];
-            red[1][threadIdx.x] += red[1][threadIdx.x + w];
-        }
-        __syncthreads();
+    Moments mo{0.0, 0.0, 0.0};
+    if (i < n) {
+        const double c = (double)T;
+        mo = Moments{c, K + s / c, fmax(s2 - s * (s / c), 0.0)};
     }
-    if (threadIdx.x == 0) {
-        partial[blockIdx.x] = red[0][0];
-        partial[gridDim.x + blockIdx.x] = red[1][0];
-    }
-}
-
-// stats[0] = count, stats[1] = sum (partial[0..nb)), stats[3] = sum of squares (partial[nb..2 nb))
-__global__ void k_gae_sums(const double* __restrict__ partial, int nb, double count, double* __restrict__ stats) {
-    __shared__ double red[2][256];
-    double s = 0.0, s2 = 0.0;
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) {
-        s += partial[k];
-        s2 += partial[nb + k];
-    }
-    red[0][threadIdx.x] = s;
-    red[1][threadIdx.x] = s2;
-    __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) {
-            red[0][threadIdx.x] += red[0][threadIdx.x + w];
-            red[1][threadIdx.x] += red[1][threadIdx.x + w];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        stats[0] = count;
-        stats[1] = red[0][0];
-        stats[3] = red[1][0];
-    }
-}
-
-// one-pass finalisation from global count / sum / sum of squares: mean, sum sq dev, unbiased std
-__global__ void k_stats_onepass(double* stats) {
-    const double c = stats[0], mean = stats[1] / c;
-    const double ssd = fmax(stats[3] - mean * stats[1], 0.0);
-    stats[2] = mean;
-    stats[3] = ssd;
-    stats[4] = sqrt(ssd / (c > 1.0 ? c - 1.0 : 1.0));
-}
-
-// block partials of sum (x - center)^2 (second pass of the normalisation)
-__global__ void k_sqdev(const float* __restrict__ x, int64_t count, const double* __restrict__ stats,
-                        double* __restrict__ partial) {
-    __shared__ double red[256];
-    const double c = stats[2];
-    double s = 0.0;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < count; k += (int64_t)gridDim.x * blockDim.x) {
-        const double d = (double)x[k] - c;
-        s += d * d;
-    }
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
+    block_merge<kGaeThreads>(mo, red);
     if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// Local moments of the rank, contiguous so ranks exchange them as one 3-element block:
+// stats[5] = count, stats[6] = mean, stats[7] = M2 (sum of squared deviations).
+__global__ void k_gae_sums(const Moments* __restrict__ partial, int nb, double* __restrict__ stats) {
+    __shared__ Moments red[256];
+    Moments a{0.0, 0.0, 0.0};
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) a = merge(a, partial[k]);
+    block_merge<256>(a, red);
+    if (threadIdx.x == 0) {
+        stats[5] = red[0].n;
+        stats[6] = red[0].mean;
+        stats[7] = red[0].m2;
+    }
+}
+
+// Global statistics from the ranks' (count, mean, M2) triples, merged in rank order:
+// stats[0] count, [1] sum, [2] mean, [3] sum of squared deviations, [4] unbiased std
+__global__ void k_stats_combine(const double* __restrict__ moments, int world, double* stats) {
+    Moments a{0.0, 0.0, 0.0};
+    for (int r = 0; r < world; ++r) a = merge(a, Moments{moments[3 * r], moments[3 * r + 1], moments[3 * r + 2]});
+    stats[0] = a.n;
+    stats[1] = a.n * a.mean;
+    stats[2] = a.mean;
+    stats[3] = a.m2;
+    stats[4] = sqrt(a.m2 / (a.n > 1.0 ? a.n - 1.0 : 1.0));
 }
 
 // out[slot] = sum(partials) (fixed order)
@@ -926,12 +931,6 @@ __global__ void k_sum_partials(const double* __restrict__ partial, int nb, doubl
     if (threadIdx.x == 0) out[slot] = red[0];
 }
 
-// stats: [0] global count, [1] sum, [2] mean, [3] sum sq dev, [4] std
-__global__ void k_stats_mean(double* stats) { stats[2] = stats[1] / stats[0]; }
-__global__ void k_stats_std(double* stats) {
-    const double c = stats[0];
-    stats[4] = sqrt(stats[3] / (c > 1.0 ? c - 1.0 : 1.0));  // unbiased (torch.std)
-}
 
 // ------------------------------------------------------------------ PPO heads
 struct HeadArgs {
@@ -1173,6 +1172,8 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
     DXRL_REQUIRE(env->cfg.reward_type == DXRL_REWARD_DENSE, "the policy-gradient rollout uses the dense reward");
     DXRL_REQUIRE(a->record_cap == 0 || (a->rec_return && a->rec_length && a->rec_success && a->rec_end_step),
                  "record_cap > 0 needs all four record buffers");
+    DXRL_REQUIRE(!a->ep_code || (a->max_steps < 16384 && env->cfg.max_episode_steps < 16383),
+                 "ep_code holds episode lengths below 2^14: max_steps / max_episode_steps too large");
     PgRolloutArgs p{env->soa,
                     weights_of(env->cfg),
                     env->cfg.max_episode_steps,
@@ -1203,7 +1204,9 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                     a->rec_return,
                     a->rec_length,
                     a->rec_success,
-                    a->rec_end_step};
+                    a->rec_end_step,
+                    a->ep_code,
+                    a->applied_act};
     DeviceGuard g(env->device);
     const int64_t n = env->cfg.num_envs;
     if (a->obs_fm || (a->diag_flags & 16)) {  // feature-major tape / A-B reference: the 64-env kernel
@@ -1245,31 +1248,25 @@ int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const flo
     hipStream_t st = as_stream(stream);
     const int nb = (int)((num_envs + kGaeThreads - 1) / kGaeThreads);
     hipLaunchKernelGGL(k_gae, dim3(nb), dim3(kGaeThreads), 0, st, rew, done, values, num_envs, horizon, (float)gamma,
-                       (float)lam, adv, ret, partial);
+                       (float)lam, adv, ret, reinterpret_cast<Moments*>(partial));
     if (int rc = launch_check("k_gae")) return rc;
-    hipLaunchKernelGGL(k_gae_sums, dim3(1), dim3(256), 0, st, partial, nb, (double)(num_envs * horizon), stats);
+    hipLaunchKernelGGL(k_gae_sums, dim3(1), dim3(256), 0, st, reinterpret_cast<const Moments*>(partial), nb, stats);
     return launch_check("k_gae_sums");
+}
+
+int dxrl_pg_adv_combine(int32_t device, const double* moments, int32_t world, double* stats, void* stream) {
+    DXRL_REQUIRE(moments && stats && world >= 1, "bad argument");
+    DeviceGuard g(device);
+    hipLaunchKernelGGL(k_stats_combine, dim3(1), dim3(1), 0, as_stream(stream), moments, world, stats);
+    return launch_check("k_stats_combine");
 }
 
 int dxrl_pg_adv_finalize(int32_t device, int32_t phase, const float* adv, int64_t count, double* partial,
                          double* stats, void* stream) {
-    DXRL_REQUIRE(adv && partial && stats, "null argument");
-    DeviceGuard g(device);
-    hipStream_t st = as_stream(stream);
-    if (phase == 0) {  // stats[1] (global sum) and stats[0] (global count) are set: mean, then sq-dev partials
-        hipLaunchKernelGGL(k_stats_mean, dim3(1), dim3(1), 0, st, stats);
-        if (int rc = launch_check("k_stats_mean")) return rc;
-        const int nb = 1024;
-        hipLaunchKernelGGL(k_sqdev, dim3(nb), dim3(256), 0, st, adv, count, stats, partial);
-        if (int rc = launch_check("k_sqdev")) return rc;
-        return reduce_to(partial, nb, stats, 3, st);
-    }
-    if (phase == 2) {  // one pass: stats[0] count, [1] sum, [3] sum of squares are global
-        hipLaunchKernelGGL(k_stats_onepass, dim3(1), dim3(1), 0, st, stats);
-        return launch_check("k_stats_onepass");
-    }
-    hipLaunchKernelGGL(k_stats_std, dim3(1), dim3(1), 0, st, stats);
-    return launch_check("k_stats_std");
+    DXRL_REQUIRE(stats, "null argument");
+    DXRL_REQUIRE(phase == 2, "phase must be 2 (the two-pass phases 0 / 1 were retired for the merged moments)");
+    (void)adv, (void)count, (void)partial;
+    return dxrl_pg_adv_combine(device, stats + 5, 1, stats, stream);
 }
 
 int dxrl_pg_heads(int32_t device, const dxrl_pg_heads_args* a, void* stream) {

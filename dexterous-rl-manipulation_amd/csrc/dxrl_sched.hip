@@ -1,0 +1,325 @@
+// dxrl_sched.hip -- the CurriculumScheduler feed on the device (config C3).
+//
+// The reference feeds its scheduler one finished episode at a time
+// (evaluation/component_ablation.py:160-170 -> experiments/curriculum_scheduler.py:116-140):
+// append (success, steps), then progress when
+//   total_episodes >= min_episodes  and  len(successes) >= window  and
+//   mean(successes[-window:]) >= threshold          (curriculum_scheduler.py:142-170)
+// and interpolate the config one 1/progression_steps notch further (:172-222).  A
+// vectorised iteration finishes up to T*N episodes per rank (700 k at 4096 envs on the
+// easy curriculum), so the feed runs here: the rollout writes one u16 code per (step,
+// env) -- 0, or (episode length << 1) | success -- and these kernels walk the codes in
+// the order the host would have fed them, (end step, global env id), across all ranks'
+// (all-gathered) tapes.  They return what the host scheduler needs to replay the batch
+// exactly: the episode / step / success totals, the first P episodes at which the
+// progression test holds (with the cumulative steps and window successes there), and the
+// new tail of the last `window` episodes.  Only those few numbers cross PCIe.
+//
+// Global order index g = t * (world N) + r N + i  ->  codes[(r T + t) N + i].
+//   k_sched_count    per 2048-code chunk: episodes, steps, successes
+//   k_sched_offsets  one workgroup: exclusive chunk offsets, totals, the tail's prefix
+//   k_sched_scatter  per chunk: episode index k of every end -> cumulative steps[k] and the
+//                    success prefix cs[tail + k + 1]
+//   k_sched_ok       per 256 episodes: the progression test, the block's first candidates
+//   k_sched_collect  one workgroup: the first P candidates overall, the new tail
+#include "dxrl_internal.h"
+
+using namespace dxrl;
+
+namespace {
+
+constexpr int kThreads = 256, kPer = 8, kChunk = kThreads * kPer;
+constexpr int kCollectThreads = 1024;
+
+struct CodeView {
+    const uint16_t* codes;
+    int64_t n, T, world, L;
+    __device__ __forceinline__ uint16_t at(int64_t g) const {
+        const int64_t wn = world * n;
+        const int64_t t = g / wn, rem = g - t * wn;
+        const int64_t r = rem / n, i = rem - r * n;
+        return codes[(r * T + t) * n + i];
+    }
+};
+
+struct Tri {
+    int64_t c, s, u;  // episodes, steps, successes
+};
+__device__ __forceinline__ Tri add(Tri a, Tri b) { return Tri{a.c + b.c, a.s + b.s, a.u + b.u}; }
+
+// exclusive scan of one Tri per thread over a workgroup (Hillis-Steele in LDS)
+template <int NT>
+__device__ Tri block_exclusive_scan(Tri v, Tri* lds, Tri& total) {
+    const int tid = threadIdx.x;
+    lds[tid] = v;
+    __syncthreads();
+    for (int d = 1; d < NT; d <<= 1) {
+        Tri o{0, 0, 0};
+        if (tid >= d) o = lds[tid - d];
+        __syncthreads();
+        if (tid >= d) lds[tid] = add(lds[tid], o);
+        __syncthreads();
+    }
+    total = lds[NT - 1];
+    Tri ex = tid ? lds[tid - 1] : Tri{0, 0, 0};
+    __syncthreads();
+    return ex;
+}
+
+__global__ __launch_bounds__(kThreads) void k_sched_count(CodeView v, Tri* blk) {
+    __shared__ Tri lds[kThreads];
+    const int64_t g0 = (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kPer;
+    Tri a{0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int64_t g = g0 + k;
+        if (g < v.L) {
+            const uint16_t x = v.at(g);
+            if (x) {
+                a.c += 1;
+                a.s += x >> 1;
+                a.u += x & 1;
+            }
+        }
+    }
+    Tri tot;
+    (void)block_exclusive_scan<kThreads>(a, lds, tot);
+    if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+}
+
+// off[b] = exclusive prefix of blk; summary[0..2] = totals; cs[0..tail_len] = tail success prefix
+__global__ __launch_bounds__(kCollectThreads) void k_sched_offsets(const Tri* blk, int nb, Tri* off,
+                                                                   const uint16_t* tail, const int32_t* tail_len,
+                                                                   int32_t* cs, int64_t* summary) {
+    __shared__ Tri lds[kCollectThreads];
+    const int per = (nb + kCollectThreads - 1) / kCollectThreads;
+    const int lo = threadIdx.x * per, hi = min(nb, lo + per);
+    Tri a{0, 0, 0};
+    for (int b = lo; b < hi; ++b) a = add(a, blk[b]);
+    Tri tot;
+    Tri run = block_exclusive_scan<kCollectThreads>(a, lds, tot);
+    for (int b = lo; b < hi; ++b) {
+        off[b] = run;
+        run = add(run, blk[b]);
+    }
+    if (threadIdx.x == 0) {
+        summary[0] = tot.c;
+        summary[1] = tot.s;
+        summary[2] = tot.u;
+        const int tl = *tail_len;
+        int32_t c = 0;
+        cs[0] = 0;
+        for (int j = 0; j < tl; ++j) {
+            c += tail[j] & 1;
+            cs[j + 1] = c;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_sched_scatter(CodeView v, const Tri* off, const int32_t* tail_len,
+                                                            int32_t* cs, int64_t* csteps) {
+    __shared__ Tri lds[kThreads];
+    const int64_t g0 = (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kPer;
+    uint16_t x[kPer];
+    Tri a{0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int64_t g = g0 + k;
+        x[k] = g < v.L ? v.at(g) : (uint16_t)0;
+        if (x[k]) {
+            a.c += 1;
+            a.s += x[k] >> 1;
+            a.u += x[k] & 1;
+        }
+    }
+    Tri tot;
+    Tri run = add(off[blockIdx.x], block_exclusive_scan<kThreads>(a, lds, tot));
+    const int tl = *tail_len;
+    const int32_t tail_succ = cs[tl];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        if (x[k]) {
+            run.s += x[k] >> 1;
+            run.u += x[k] & 1;
+            csteps[run.c] = run.s;                            // steps through episode k = run.c
+            cs[tl + run.c + 1] = tail_succ + (int32_t)run.u;  // successes through history index tl + k
+            run.c += 1;
+        }
+    }
+}
+
+struct OkParams {
+    int32_t window;
+    double threshold;
+    int64_t min_episodes, episodes_before;
+};
+
+__device__ __forceinline__ int32_t window_successes(const int32_t* cs, int tl, int64_t k, int32_t w) {
+    const int64_t e = tl + k + 1;  // history prefix length through episode k
+    const int64_t b = e - w > 0 ? e - w : 0;
+    return cs[e] - cs[b];
+}
+
+__device__ __forceinline__ bool progression_test(const OkParams& q, int64_t k, int32_t win) {
+    const int64_t total = q.episodes_before + k + 1;  // total_episodes == len(episode_successes)
+    return total >= q.min_episodes && total >= q.window && (double)win / (double)q.window >= q.threshold;
+}
+
+// one thread per episode; per 256-episode block: number of candidates and the first kCap of them
+template <int kCap>
+__global__ __launch_bounds__(kThreads) void k_sched_ok(const int64_t* summary, const int32_t* tail_len,
+                                                       const int32_t* cs, OkParams q, int32_t* okcnt,
+                                                       int64_t* okfirst) {
+    __shared__ int wave_cnt[kThreads / 64];
+    const int64_t E = summary[0];
+    const int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const int tl = *tail_len;
+    bool ok = false;
+    if (k < E) ok = progression_test(q, k, window_successes(cs, tl, k, q.window));
+    const unsigned long long m = __ballot(ok);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) wave_cnt[wave] = __popcll(m);
+    __syncthreads();
+    int before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) {
+        before += w < wave ? wave_cnt[w] : 0;
+        total += wave_cnt[w];
+    }
+    if (ok) {
+        const int rank = before + __popcll(m & ((1ull << lane) - 1ull));
+        if (rank < kCap) okfirst[(int64_t)blockIdx.x * kCap + rank] = k;
+    }
+    if (threadIdx.x == 0) okcnt[blockIdx.x] = total;
+}
+
+// the first P candidates in episode order (P <= kCap), their cumulative steps and window
+// successes; the new tail = the last min(window, tail_len + E) history codes
+template <int kCap>
+__global__ __launch_bounds__(kCollectThreads) void k_sched_collect(
+    int nb, int32_t P, const int32_t* okcnt, const int64_t* okfirst, const int32_t* cs, const int64_t* csteps,
+    int32_t window, const uint16_t* tail_in, const int32_t* tail_len_in, uint16_t* tail_out, int32_t* tail_len_out,
+    int64_t* summary) {
+    __shared__ int64_t lds[kCollectThreads];
+    __shared__ int64_t found_total;
+    const int per = (nb + kCollectThreads - 1) / kCollectThreads;
+    const int lo = threadIdx.x * per, hi = min(nb, lo + per);
+    int64_t a = 0;
+    for (int b = lo; b < hi; ++b) a += okcnt[b];
+    lds[threadIdx.x] = a;
+    __syncthreads();
+    for (int d = 1; d < kCollectThreads; d <<= 1) {
+        const int64_t o = threadIdx.x >= d ? lds[threadIdx.x - d] : 0;
+        __syncthreads();
+        lds[threadIdx.x] += o;
+        __syncthreads();
+    }
+    int64_t run = threadIdx.x ? lds[threadIdx.x - 1] : 0;
+    if (threadIdx.x == kCollectThreads - 1) found_total = lds[kCollectThreads - 1];
+    const int tl = *tail_len_in;
+    for (int b = lo; b < hi && run < P; ++b) {
+        const int c = okcnt[b];
+        for (int j = 0; j < c && j < kCap && run + j < P; ++j) {
+            const int64_t k = okfirst[(int64_t)b * kCap + j];
+            int64_t* o = summary + 4 + 3 * (run + j);
+            o[0] = k;
+            o[1] = csteps[k];
+            o[2] = window_successes(cs, tl, k, window);
+        }
+        run += c;
+    }
+    __syncthreads();
+    const int64_t E = summary[0];
+    if (threadIdx.x == 0) summary[3] = found_total < P ? found_total : P;
+    const int64_t hist = tl + E;
+    const int32_t nl = (int32_t)(hist < window ? hist : window);
+    for (int j = threadIdx.x; j < nl; j += kCollectThreads) {
+        const int64_t x = hist - nl + j;  // history index
+        uint16_t code;
+        if (x < tl) {
+            code = tail_in[x];
+        } else {
+            const int64_t k = x - tl;
+            const int64_t len = csteps[k] - (k ? csteps[k - 1] : 0);
+            code = (uint16_t)((len << 1) | (int64_t)(cs[x + 1] - cs[x]));
+        }
+        tail_out[j] = code;
+    }
+    if (threadIdx.x == 0) *tail_len_out = nl;
+}
+
+constexpr int kCap = DXRL_SCHED_MAX_CANDIDATES;
+
+struct Scratch {
+    Tri* blk;
+    Tri* off;
+    int32_t* cs;
+    int64_t* csteps;
+    int32_t* okcnt;
+    int64_t* okfirst;
+    size_t bytes;
+};
+
+Scratch carve(char* base, int64_t L, int32_t window) {
+    const int64_t nb = (L + kChunk - 1) / kChunk, nb4 = (L + kThreads - 1) / kThreads;
+    Scratch s{};
+    size_t o = 0;
+    const auto take = [&](size_t bytes) {
+        char* p = base ? base + o : nullptr;
+        o += (bytes + 255) & ~(size_t)255;
+        return p;
+    };
+    s.blk = reinterpret_cast<Tri*>(take(sizeof(Tri) * (size_t)nb));
+    s.off = reinterpret_cast<Tri*>(take(sizeof(Tri) * (size_t)nb));
+    s.cs = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (size_t)(window + L + 1)));
+    s.csteps = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * (size_t)(L > 0 ? L : 1)));
+    s.okcnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (size_t)(nb4 > 0 ? nb4 : 1)));
+    s.okfirst = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * (size_t)kCap * (size_t)(nb4 > 0 ? nb4 : 1)));
+    s.bytes = o;
+    return s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dxrl_sched_scratch_bytes(int32_t world, int32_t horizon, int64_t num_envs, int32_t window, int64_t* bytes) {
+    DXRL_REQUIRE(bytes && world >= 1 && horizon >= 1 && num_envs >= 1 && window >= 1, "bad scheduler-scan shape");
+    *bytes = (int64_t)carve(nullptr, (int64_t)world * horizon * num_envs, window).bytes;
+    return DXRL_OK;
+}
+
+int dxrl_sched_scan(int32_t device, const dxrl_sched_args* a, void* stream) {
+    DXRL_REQUIRE(a && a->codes && a->tail_in && a->tail_out && a->tail_len_in && a->tail_len_out && a->scratch &&
+                     a->summary,
+                 "null argument");
+    DXRL_REQUIRE(a->world >= 1 && a->horizon >= 1 && a->num_envs >= 1, "bad codes shape");
+    DXRL_REQUIRE(a->window >= 1, "window must be >= 1");
+    DXRL_REQUIRE(a->max_candidates >= 0 && a->max_candidates <= kCap, "max_candidates outside [0, %d]", kCap);
+    DXRL_REQUIRE(a->tail_in != a->tail_out, "tail_in and tail_out must differ");
+    const int64_t L = (int64_t)a->world * a->horizon * a->num_envs;
+    Scratch s = carve(static_cast<char*>(a->scratch), L, a->window);
+    DXRL_REQUIRE(a->scratch_bytes >= (int64_t)s.bytes, "scratch too small: %lld < %lld bytes",
+                 (long long)a->scratch_bytes, (long long)s.bytes);
+    DeviceGuard g(device);
+    hipStream_t st = as_stream(stream);
+    const CodeView v{a->codes, a->num_envs, a->horizon, a->world, L};
+    const int nb = (int)((L + kChunk - 1) / kChunk), nb4 = (int)((L + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(k_sched_count, dim3(nb), dim3(kThreads), 0, st, v, s.blk);
+    if (int rc = launch_check("k_sched_count")) return rc;
+    hipLaunchKernelGGL(k_sched_offsets, dim3(1), dim3(kCollectThreads), 0, st, s.blk, nb, s.off, a->tail_in,
+                       a->tail_len_in, s.cs, a->summary);
+    if (int rc = launch_check("k_sched_offsets")) return rc;
+    hipLaunchKernelGGL(k_sched_scatter, dim3(nb), dim3(kThreads), 0, st, v, s.off, a->tail_len_in, s.cs, s.csteps);
+    if (int rc = launch_check("k_sched_scatter")) return rc;
+    const OkParams q{a->window, a->threshold, a->min_episodes, a->episodes_before};
+    hipLaunchKernelGGL(k_sched_ok<kCap>, dim3(nb4), dim3(kThreads), 0, st, a->summary, a->tail_len_in, s.cs, q,
+                       s.okcnt, s.okfirst);
+    if (int rc = launch_check("k_sched_ok")) return rc;
+    hipLaunchKernelGGL(k_sched_collect<kCap>, dim3(1), dim3(kCollectThreads), 0, st, nb4, a->max_candidates,
+                       s.okcnt, s.okfirst, s.cs, s.csteps, a->window, a->tail_in, a->tail_len_in, a->tail_out,
+                       a->tail_len_out, a->summary);
+    return launch_check("k_sched_collect");
+}
+
+}  // extern "C"

@@ -261,6 +261,16 @@ class VecEnv:
         return self._view(self.layout.friction, self.num_envs, torch.float64, (self.num_envs,))
 
     @property
+    def curriculum_index(self):
+        """Row of ``curriculum_configs`` each env resets from (i32 [N])."""
+        return self._view(self.layout.cfg_index, self.num_envs, torch.int32, (self.num_envs,))
+
+    @property
+    def reset_counter(self):
+        """Philox counter of each env's next device-RNG reset (u64 [N], as int64)."""
+        return self._view(self.layout.reset_ctr, self.num_envs, torch.int64, (self.num_envs,))
+
+    @property
     def contacts(self):
         bits = self.flags & 0xFF
         return torch.stack([(bits >> f) & 1 for f in range(NUM_FINGERS)], dim=1).to(torch.float32)

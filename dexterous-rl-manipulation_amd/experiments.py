@@ -140,11 +140,20 @@ class CurriculumConfig:
 
 # ============================================================ curriculum schedulers
 class CurriculumScheduler:
-    """Success-rate driven difficulty progression (curriculum_scheduler.py:13-273)."""
+    """Success-rate driven difficulty progression (curriculum_scheduler.py:13-273).
+
+    ``history``: "full" keeps every episode in ``episode_successes`` / ``episode_steps``
+    as the reference does; "window" keeps only the last ``window_size`` of them (all the
+    progression rule reads) plus counters, so a vectorised trainer feeding ~10^5-10^6
+    episodes per iteration (``apply_device_summary``) does not grow host lists.  Totals,
+    statistics and progression points are identical in both modes."""
 
     def __init__(self, initial_config: CurriculumConfig, target_config: CurriculumConfig,
                  success_rate_threshold: float = 0.7, min_episodes_before_progression: int = 50,
-                 window_size: int = 20, progression_steps: int = 5):
+                 window_size: int = 20, progression_steps: int = 5, history: str = "full"):
+        if history not in ("full", "window"):
+            raise ValueError("history must be 'full' or 'window'")
+        self.history = history
         self.initial_config = initial_config
         self.target_config = target_config
         self.success_rate_threshold = success_rate_threshold
@@ -182,7 +191,23 @@ class CurriculumScheduler:
         self.episode_steps.append(episode_steps)
         self.total_steps += episode_steps
         self.total_episodes += 1
-        return self._progress() if self._should_progress() else False
+        self._n_success += bool(success)
+        progressed = self._progress() if self._should_progress() else False
+        self._trim()
+        return progressed
+
+    def _trim(self):
+        if self.history == "window" and len(self.episode_successes) > self.window_size:
+            del self.episode_successes[:-self.window_size]
+            del self.episode_steps[:-self.window_size]
+
+    def _uses_success_window_rule(self) -> bool:
+        """True when update / _should_progress / _progress are this class's (the rule the
+        vectorised paths restate); subclasses such as StepBasedScheduler are fed per episode
+        or through their own update_batch."""
+        t = type(self)
+        return (t.update is CurriculumScheduler.update and t._should_progress is CurriculumScheduler._should_progress
+                and t._progress is CurriculumScheduler._progress and self.window_size > 0)
 
     def update_batch(self, successes, episode_steps) -> bool:
         """Exactly ``any([self.update(s, n) for s, n in zip(successes, episode_steps)])`` --
@@ -198,9 +223,9 @@ class CurriculumScheduler:
         if n == 0:
             return False
         w = self.window_size
-        if w <= 0 or type(self).update is not CurriculumScheduler.update:  # other rules: per-episode calls
+        if not self._uses_success_window_rule():  # other rules: per-episode calls
             return any([self.update(bool(a), int(b)) for a, b in zip(s, st)])
-        base = len(self.episode_successes)
+        base = self.total_episodes  # == len(episode_successes) with history="full"
         tail = np.asarray(self.episode_successes[-w:] if w > 0 else [], dtype=bool)
         hist = np.concatenate([tail, s])
         csum = np.concatenate([[0], np.cumsum(hist, dtype=np.int64)])
@@ -218,12 +243,60 @@ class CurriculumScheduler:
             self.episode_steps.extend(st[done:j + 1].tolist())
             self.total_steps += int(steps_cum[j] - (steps_cum[done - 1] if done else 0))
             self.total_episodes += int(j + 1 - done)
+            self._n_success += int(s[done:j + 1].sum())
             done = int(j + 1)
-            progressed |= self._progress()
+            progressed |= self._progress(rate=float(cnt[j]) / w)
         self.episode_successes.extend(s[done:].tolist())
         self.episode_steps.extend(st[done:].tolist())
         self.total_steps += int(steps_cum[-1] - (steps_cum[done - 1] if done else 0))
         self.total_episodes += int(n - done)
+        self._n_success += int(s[done:].sum())
+        self._trim()
+        return progressed
+
+    def remaining_progressions(self, cap: int) -> int:
+        """How many more _progress calls can raise the level (at most cap + 1 is reported)."""
+        lvl, n = self.current_difficulty_level, 0
+        while lvl < 1.0 and n <= cap:
+            new = min(lvl + 1.0 / self.progression_steps, 1.0)
+            if new <= lvl:
+                break
+            lvl, n = new, n + 1
+        return n
+
+    def apply_device_summary(self, episodes: int, steps: int, successes: int, candidates, tail_codes,
+                             episode_codes=None) -> bool:
+        """Replay a batch summarised on the device (csrc/dxrl_sched.hip, dxrl_sched_scan):
+        ``candidates`` = [(k, steps through k, window successes at k)] are the first episodes of
+        the batch at which the progression test holds, in order; ``tail_codes`` the batch's
+        last min(window, episodes) codes ((length << 1) | success) (history="window");
+        ``episode_codes`` (history="full") every code of the batch.  Same totals, progression
+        points and history entries as ``update_batch`` over the batch's (success, steps)."""
+        if not self._uses_success_window_rule():
+            raise ValueError("apply_device_summary restates CurriculumScheduler's success-window rule only")
+        w = self.window_size
+        e0, s0 = self.total_episodes, self.total_steps
+        progressed = False
+        for k, st_k, win in candidates:
+            if self.current_difficulty_level >= 1.0:
+                break
+            self.total_episodes = e0 + int(k) + 1
+            self.total_steps = s0 + int(st_k)
+            progressed |= self._progress(rate=float(win) / w)
+        self.total_episodes = e0 + int(episodes)
+        self.total_steps = s0 + int(steps)
+        self._n_success += int(successes)
+        if episode_codes is not None:
+            codes = np.asarray(episode_codes, dtype=np.int64)
+            self.episode_successes.extend((codes & 1).astype(bool).tolist())
+            self.episode_steps.extend((codes >> 1).tolist())
+        else:
+            if self.history == "full":
+                raise ValueError("history='full' needs every episode code of the batch")
+            tail = np.asarray(tail_codes, dtype=np.int64)[len(tail_codes) - min(w, int(episodes)):]
+            self.episode_successes.extend((tail & 1).astype(bool).tolist())
+            self.episode_steps.extend((tail >> 1).tolist())
+        self._trim()
         return progressed
 
     def _window_rate(self):
@@ -234,17 +307,20 @@ class CurriculumScheduler:
             return False
         if self.current_difficulty_level >= 1.0:
             return False
-        if len(self.episode_successes) < self.window_size:
+        if self.total_episodes < self.window_size:  # == len(episode_successes) with history="full"
             return False
         return self._window_rate() >= self.success_rate_threshold
 
-    def _progress(self) -> bool:
+    def _progress(self, rate: Optional[float] = None) -> bool:
+        """rate: the window success rate at this episode when the caller already has it
+        (vectorised feeds); otherwise read from the list, as the reference does."""
         new = min(self.current_difficulty_level + 1.0 / self.progression_steps, 1.0)
         if new <= self.current_difficulty_level:
             return False
         self.current_difficulty_level = new
         self.current_config = self._interpolate_config(new)
-        self.progression_history.append(self._history_entry(success_rate=float(self._window_rate())))
+        self.progression_history.append(
+            self._history_entry(success_rate=float(self._window_rate()) if rate is None else float(rate)))
         return True
 
     def _history_entry(self, **extra):
@@ -263,14 +339,14 @@ class CurriculumScheduler:
         return self.current_difficulty_level
 
     def get_statistics(self) -> Dict:
-        n = len(self.episode_successes)
+        n = self.total_episodes
         recent = self.episode_successes[-self.window_size:] if n >= self.window_size else self.episode_successes
         return {
             "total_episodes": self.total_episodes,
             "total_steps": self.total_steps,
             "current_difficulty_level": float(self.current_difficulty_level),
             "recent_success_rate": float(np.mean(recent)) if recent else 0.0,
-            "overall_success_rate": float(np.mean(self.episode_successes)) if n else 0.0,
+            "overall_success_rate": self._n_success / n if n else 0.0,  # == np.mean(all successes)
             "num_progressions": len(self.progression_history),
             "progression_history": list(self.progression_history),
         }
@@ -282,6 +358,7 @@ class CurriculumScheduler:
         self.episode_steps: List[int] = []
         self.total_steps = 0
         self.total_episodes = 0
+        self._n_success = 0
         self.progression_history: List[Dict] = []
 
 
@@ -297,7 +374,47 @@ class StepBasedScheduler(CurriculumScheduler):
         return (self.current_milestone_idx < len(self.step_milestones)
                 and self.total_steps >= self.step_milestones[self.current_milestone_idx])
 
-    def _progress(self) -> bool:
+    def update_batch(self, successes, episode_steps) -> bool:
+        """Exactly ``any([self.update(s, n) for ...])``: update() tests once per episode, so a
+        milestone fires at the first episode whose running step total reaches it and at most
+        one milestone fires per episode (the next one at a later episode at the earliest)."""
+        t = type(self)
+        if (t.update is not CurriculumScheduler.update or t._should_progress is not StepBasedScheduler._should_progress
+                or t._progress is not StepBasedScheduler._progress):
+            return super().update_batch(successes, episode_steps)
+        s = np.asarray(successes, dtype=bool).ravel()
+        st = np.asarray(episode_steps, dtype=np.int64).ravel()
+        if s.shape != st.shape:
+            raise ValueError("successes and episode_steps must have the same length")
+        n = s.size
+        if n == 0:
+            return False
+        cum = self.total_steps + np.cumsum(st)
+        fire, j_prev = [], -1
+        for m in self.step_milestones[self.current_milestone_idx:]:
+            j = max(int(np.searchsorted(cum, m, side="left")), j_prev + 1)
+            if j >= n:
+                break
+            fire.append(j)
+            j_prev = j
+        done, progressed = 0, False
+        for j in fire:
+            self.episode_successes.extend(s[done:j + 1].tolist())
+            self.episode_steps.extend(st[done:j + 1].tolist())
+            self.total_steps = int(cum[j])
+            self.total_episodes += int(j + 1 - done)
+            self._n_success += int(s[done:j + 1].sum())
+            done = j + 1
+            progressed |= self._progress()
+        self.episode_successes.extend(s[done:].tolist())
+        self.episode_steps.extend(st[done:].tolist())
+        self.total_steps = int(cum[-1])
+        self.total_episodes += int(n - done)
+        self._n_success += int(s[done:].sum())
+        self._trim()
+        return progressed
+
+    def _progress(self, rate: Optional[float] = None) -> bool:
         if self.current_milestone_idx >= len(self.step_milestones):
             return False
         self.current_milestone_idx += 1

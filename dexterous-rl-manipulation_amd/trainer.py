@@ -9,8 +9,9 @@ actor-critic with GAE and policy gradients on top of the same env.  One
      the step kernel (bf16 MFMA), Gaussian sampling, optional fused noise
      injection (robustness_tests.py:140-211), auto-reset, training tape;
   2. critic forward over the T+1 observation blocks (bf16 MFMA GEMMs);
-  3. ``dxrl_pg_gae`` reverse scan + one-pass (f64 moments) advantage normalisation
-     (global across ranks: two 1-element all-reduces);
+  3. ``dxrl_pg_gae`` reverse scan + advantage normalisation from (count, mean, M2)
+     moments merged without cancellation (global across ranks: one all-gather of each
+     rank's 3 f64, merged in rank order by ``dxrl_pg_adv_combine``);
   4. actor forward, PPO-clip / value / entropy heads (``dxrl_pg_heads``);
   5. backward GEMMs (input grads with fused tanh' gate, weight grads by
      split-K over samples with the bias as an extra ones-row);
@@ -30,7 +31,7 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .distributed import all_reduce_sum_
+from .distributed import all_gather_into_, all_reduce_sum_, gather_adv_moments_, global_count, loss_scales
 from .envs import VecEnv
 
 # csrc/dxrl_pg.h
@@ -96,6 +97,7 @@ class PGTrainer:
         self.max_steps = cfg.max_steps or env.max_episode_steps
         self.pg = process_group
         self.world = world_size
+        self.global_M = global_count(self.M, self.world, self.pg)  # samples of all ranks per iteration
         self.step_count = 0
         self.iteration_index = 0
         self.diag_flags = 0  # rollout timing ablations only (see dxrl_pg_rollout_args.diag_flags)
@@ -122,6 +124,7 @@ class PGTrainer:
         if cfg.success_rule not in ("training", "terminated"):
             raise ValueError("success_rule must be 'training' or 'terminated'")
         self.scheduler = None
+        self.ep_code = None  # u16 [T N] episode-end codes (scheduler feed, attach_curriculum)
         # hidden activations, row-major [rows][288]: columns 0..255 = tanh units, column 256 = 1
         # (the next layer reads K = 256; the weight-gradient GEMM reads I = 288 and gets the bias
         # gradient as column 256)
@@ -133,7 +136,8 @@ class PGTrainer:
         self.V = z(OUT, (T + 1) * n)
         self.adv, self.ret = z(M), z(M)
         self.stats = torch.zeros(8, dtype=torch.float64, device=d)
-        nb = max(1024, (M + 255) // 256, 2 * ((n + 63) // 64))  # GAE: 2 moments per 64-env block
+        self.moments_all = torch.zeros(self.world, 3, dtype=torch.float64, device=d)  # ranks' stats[5..7]
+        nb = max(1024, (M + 255) // 256, 3 * ((n + 63) // 64))  # GAE: one (n, mean, M2) per 64-env block
         self.partial = torch.zeros(nb, dtype=torch.float64, device=d)
         self.dmu_rm, self.dv_rm = z(M, OUT, dt=bf), z(M, OUT, dt=bf)
         self.dls_partial = z((M + 255) // 256, ACT_PAD)
@@ -207,6 +211,8 @@ class PGTrainer:
         a.record_cap = max(0, int(self.cfg.record_cap))
         a.rec_return, a.rec_length = p(self.rec_return), p(self.rec_length)
         a.rec_success, a.rec_end_step = p(self.rec_success), p(self.rec_end)
+        a.ep_code = p(self.ep_code)
+        a.applied_act = p(getattr(self, "applied_act", None))
         N.call("dxrl_pg_rollout", self.env.handle, p(self.packed), p(self.params), C.byref(a), self._s())
 
     def _mlp_forward(self, net, rows, H1, H2, head_f32=None, head_fm=None, ld_head_fm=0):
@@ -231,8 +237,8 @@ class PGTrainer:
         f.net, f.train, f.rows = net, int(train), rows
         f.packed, f.params, f.obs = p(self.packed), p(self.params), p(self.obs_rm)
         f.act, f.logp_old, f.adv, f.ret, f.stats = p(self.act), p(self.logp), p(self.adv), p(self.ret), p(self.stats)
-        f.inv_total_samples = 1.0 / (self.M * self.world)
-        f.clip_eps, f.vf_coef, f.ent_coef = c.clip_eps, c.vf_coef, c.ent_coef / self.world
+        f.inv_total_samples, f.ent_coef = loss_scales(self.global_M, self.world, c.ent_coef)
+        f.clip_eps, f.vf_coef = c.clip_eps, c.vf_coef
         f.values = p(self.V[0])
         f.h1, f.dh2 = p(self.H1a), p(self.dH2)
         f.partial, f.loss_partial, f.grid = p(self.fused_partial), p(self.fused_loss), self.fused_grid
@@ -253,8 +259,12 @@ class PGTrainer:
     def phases(self):
         """The iteration's launch groups in order (bench.py times each)."""
         if self.cfg.fused:
-            return ["rollout", "critic_values", "advantages", "actor_train", "critic_train", "optimizer_step"]
-        return ["rollout", "critic_forward", "advantages", "actor_forward", "heads", "backward", "optimizer_step"]
+            ph = ["rollout", "critic_values", "advantages", "actor_train", "critic_train", "optimizer_step"]
+        else:
+            ph = ["rollout", "critic_forward", "advantages", "actor_forward", "heads", "backward", "optimizer_step"]
+        if self.scheduler is not None:  # feed launched behind the rollout, applied after the learner
+            ph = ph[:1] + ["schedule_feed"] + ph[1:] + ["schedule_apply"]
+        return ph
 
     def _allreduce(self, t):
         all_reduce_sum_(t, self.world, self.pg)
@@ -263,10 +273,13 @@ class PGTrainer:
         c = self.cfg
         N.call("dxrl_pg_gae", self.dev.index, N.ptr(self.rew), N.ptr(self.done), N.ptr(self.V[0]), self.n, self.T,
                c.gamma, c.lam, N.ptr(self.adv), N.ptr(self.ret), N.ptr(self.partial), N.ptr(self.stats), self._s())
-        # count, sum and sum of squares in one all-reduce, then mean / std on device (one pass, f64)
-        self._allreduce(self.stats[0:4])
-        N.call("dxrl_pg_adv_finalize", self.dev.index, 2, N.ptr(self.adv), self.M, N.ptr(self.partial),
-               N.ptr(self.stats), self._s())
+        # every rank's (count, mean, M2) in rank order, merged on device (identical on all ranks)
+        if self.world == 1:
+            N.call("dxrl_pg_adv_combine", self.dev.index, N.ptr(self.stats[5:]), 1, N.ptr(self.stats), self._s())
+        else:
+            gather_adv_moments_(self.moments_all, self.stats, self.world, self.pg)
+            N.call("dxrl_pg_adv_combine", self.dev.index, N.ptr(self.moments_all), self.world, N.ptr(self.stats),
+                   self._s())
 
     def heads(self):
         c, p = self.cfg, N.ptr
@@ -274,8 +287,8 @@ class PGTrainer:
         h.mu, h.values, h.act, h.logp_old = p(self.mu), p(self.V[0]), p(self.act), p(self.logp)
         h.adv, h.ret, h.stats, h.params = p(self.adv), p(self.ret), p(self.stats), p(self.params)
         h.num_samples = self.M
-        h.inv_total_samples = 1.0 / (self.M * self.world)
-        h.clip_eps, h.vf_coef, h.ent_coef = c.clip_eps, c.vf_coef, c.ent_coef / self.world
+        h.inv_total_samples, h.ent_coef = loss_scales(self.global_M, self.world, c.ent_coef)
+        h.clip_eps, h.vf_coef = c.clip_eps, c.vf_coef
         h.dmu_rm, h.dmu_fm, h.dv_rm, h.dv_fm = p(self.dmu_rm), None, p(self.dv_rm), None
         h.dlogstd_partial, h.loss_partial, h.grads = p(self.dls_partial), p(self.loss_partial), p(self.grads)
         N.call("dxrl_pg_heads", self.dev.index, C.byref(h), self._s())
@@ -301,32 +314,111 @@ class PGTrainer:
         self.pack()
 
     def attach_curriculum(self, scheduler):
-        """Host-side CurriculumScheduler (experiments/curriculum_scheduler.py) fed with this
-        iteration's finished episodes in (end step, global env id) order; a progression pushes
-        the new config into the device table (effective at each env's next reset, as
-        evaluation/component_ablation.py:165-166 does between episodes)."""
-        if self.cfg.record_cap <= 0:
-            raise ValueError("attach_curriculum needs TrainerConfig.record_cap > 0")
+        """Host-side CurriculumScheduler (experiments/curriculum_scheduler.py) fed with every
+        episode the iteration finished, on all ranks, in (end step, global env id) order -- the
+        order evaluation/component_ablation.py:160-170 feeds one process's episodes in.  A
+        progression pushes the new config into the device table (effective at each env's next
+        reset, as component_ablation.py:165-166 swaps it between episodes).
+
+        The rollout writes one u16 episode-end code per (step, env); ranks all-gather them
+        (RCCL) and dxrl_sched_scan walks them on the device.  With history="window" and the
+        base success-window rule only a few numbers cross PCIe (apply_device_summary);
+        otherwise (history="full", StepBasedScheduler, > 64 pending progressions) the codes
+        are copied to the host and fed through update_batch.  Either way every rank's
+        scheduler sees the same global stream, so all ranks progress together."""
         self.scheduler = scheduler
         self.env.set_curriculum(scheduler.get_current_config())
+        d, n, T = self.dev, self.n, self.T
+        self.ep_code = torch.zeros(T * n, dtype=torch.int16, device=d)
+        self.codes_all = self.ep_code if self.world == 1 else torch.zeros(self.world * T * n, dtype=torch.int16,
+                                                                          device=d)
+        w = max(1, int(scheduler.window_size))
+        self._sched_w = w
+        self._tail_dev = torch.zeros(2, w, dtype=torch.int16, device=d)
+        self._tail_len_dev = torch.zeros(2, dtype=torch.int32, device=d)
+        self._tail_in_host = torch.zeros(w, dtype=torch.int16).pin_memory()
+        self._tail_len_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        nb = C.c_int64()
+        N.call("dxrl_sched_scratch_bytes", self.world, T, n, w, C.byref(nb))
+        self._sched_scratch = torch.empty(nb.value, dtype=torch.uint8, device=d)
+        self._summary = torch.zeros(4 + 3 * N.SCHED_MAX_CANDIDATES, dtype=torch.int64, device=d)
+        self._summary_host = torch.zeros_like(self._summary, device="cpu").pin_memory()
+        self._tail_out_host = torch.zeros(w, dtype=torch.int16).pin_memory()
+        self._codes_host = None
+        self._sched_event = torch.cuda.Event()
+        self._sched_mode = None
+
+    def schedule_feed(self):
+        """Behind the rollout: all-gather the episode-end codes, scan them on the device and
+        start the (tiny) summary copy; schedule_apply() consumes it after the learner."""
+        sc = self.scheduler
+        all_gather_into_(self.codes_all, self.ep_code, self.world, self.pg)
+        P = sc.remaining_progressions(N.SCHED_MAX_CANDIDATES)
+        if sc.history == "window" and sc._uses_success_window_rule() and P <= N.SCHED_MAX_CANDIDATES:
+            w = self._sched_w
+            # the host lists are authoritative for the window carried in (success bits are all
+            # the scan reads); pinned staging, so the copies queue behind the rollout without a
+            # host sync (the previous iteration's copies finished before its schedule_apply)
+            tail = sc.episode_successes[-w:]
+            self._tail_len_host[0] = len(tail)
+            if tail:
+                self._tail_in_host[:len(tail)] = torch.tensor(tail, dtype=torch.int16)
+            self._tail_dev[0].copy_(self._tail_in_host, non_blocking=True)
+            self._tail_len_dev[0:1].copy_(self._tail_len_host, non_blocking=True)
+            a = N.SchedArgs()
+            a.codes, a.world, a.horizon, a.num_envs = N.ptr(self.codes_all), self.world, self.T, self.n
+            a.window, a.max_candidates, a.threshold = w, P, float(sc.success_rate_threshold)
+            a.min_episodes, a.episodes_before = int(sc.min_episodes_before_progression), int(sc.total_episodes)
+            a.tail_in, a.tail_len_in = N.ptr(self._tail_dev[0]), N.ptr(self._tail_len_dev[0:1])
+            a.tail_out, a.tail_len_out = N.ptr(self._tail_dev[1]), N.ptr(self._tail_len_dev[1:2])
+            a.scratch, a.scratch_bytes, a.summary = N.ptr(self._sched_scratch), self._sched_scratch.numel(), \
+                N.ptr(self._summary)
+            N.call("dxrl_sched_scan", self.dev.index, C.byref(a), self._s())
+            self._summary_host.copy_(self._summary, non_blocking=True)
+            self._tail_out_host.copy_(self._tail_dev[1], non_blocking=True)
+            self._sched_mode = "device"
+        else:
+            if self._codes_host is None:
+                self._codes_host = torch.zeros(self.codes_all.numel(), dtype=torch.int16).pin_memory()
+            self._codes_host.copy_(self.codes_all, non_blocking=True)
+            self._sched_mode = "host"
+        self._sched_event.record(torch.cuda.current_stream(self.dev))
+
+    def schedule_apply(self):
+        """Replay the iteration's episodes into the scheduler; push a progression to the env."""
+        sc = self.scheduler
+        self._sched_event.synchronize()
+        if self._sched_mode == "device":
+            s = self._summary_host.numpy()
+            E, S, U, found = (int(x) for x in s[:4])
+            cands = s[4:4 + 3 * found].reshape(found, 3)
+            w = self._sched_w
+            nl = min(w, len(sc.episode_successes[-w:]) + E)
+            tail = self._tail_out_host.numpy().view(np.uint16)[:nl][nl - min(w, E):]
+            progressed = sc.apply_device_summary(E, S, U, cands, tail)
+        else:
+            codes = self._codes_host.numpy().view(np.uint16).reshape(self.world, self.T, self.n)
+            ep = codes.transpose(1, 0, 2).ravel()
+            ep = ep[ep != 0].astype(np.int64)
+            progressed = sc.update_batch((ep & 1).astype(bool), ep >> 1)
+        if progressed:
+            self.env.set_curriculum(sc.get_current_config())
 
     def episode_records(self):
         from .training import gather_records
-        return gather_records(self.ep_count, self.cfg.record_cap, self.rec_return, self.rec_length,
-                              self.rec_success, self.rec_end, self.env._cfg.global_env_offset)
-
-    def _feed_scheduler(self):
-        rec = self.episode_records()
-        if self.scheduler.update_batch(rec.success, rec.steps):
-            self.env.set_curriculum(self.scheduler.get_current_config())
+        rec = gather_records(self.ep_count, self.cfg.record_cap, self.rec_return, self.rec_length,
+                             self.rec_success, self.rec_end, self.env._cfg.global_env_offset)
+        if rec.dropped:
+            import warnings
+            warnings.warn(f"{rec.dropped} finished episodes did not fit TrainerConfig.record_cap="
+                          f"{self.cfg.record_cap} records per env (an env can finish up to horizon="
+                          f"{self.T} episodes per iteration)", RuntimeWarning, stacklevel=2)
         return rec
 
     def iteration(self, update: bool = True):
         for name in self.phases():
             if name != "optimizer_step" or update:
                 getattr(self, name)()
-        if self.scheduler is not None:
-            self._feed_scheduler()
         self.iteration_index += 1
 
     # ------------------------------------------------------------------ stats

@@ -252,6 +252,11 @@ typedef struct dxrl_pg_rollout_args {
     int32_t* rec_length;
     uint8_t* rec_success;
     int32_t* rec_end_step;     /* step index t within this call                            */
+    uint16_t* ep_code;         /* u16 [T N] episode-end codes for the curriculum scheduler feed
+                                  (dxrl_sched_scan): 0 = no episode ended at this step, else
+                                  (episode length << 1) | success (nullable)                  */
+    float* applied_act;        /* f32 [T N][16] the action the env integrated, after dynamics
+                                  noise (nullable; parity checks replay it on the CPU)        */
 } dxrl_pg_rollout_args;
 
 /* Fused policy + env rollout: T steps of actor MLP (bf16 MFMA) -> Gaussian
@@ -259,18 +264,55 @@ typedef struct dxrl_pg_rollout_args {
 int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, const dxrl_pg_rollout_args* args,
                     void* stream);
 
-/* GAE reverse scan; values f32 [(T+1) N]; writes adv/ret [T N] and the local moments
- * stats[0] = T N, stats[1] = sum(adv), stats[3] = sum(adv^2) (partial: f64 [2 ceil(N / 64)]). */
+/* GAE reverse scan; values f32 [(T+1) N]; writes adv/ret [T N] and this rank's advantage
+ * moments stats[5] = T N, stats[6] = mean(adv), stats[7] = sum of squared deviations
+ * (per-env sums about the env's own first value, merged with Chan et al.'s pairwise update
+ * in a fixed order: no sum(a^2) - mean sum(a) cancellation).  partial: f64 [3 ceil(N / 64)];
+ * stats: f64 [8]. */
 int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const float* values, int64_t num_envs,
                 int64_t horizon, double gamma, double lam, float* adv, float* ret, double* partial, double* stats,
                 void* stream);
-/* Advantage normalisation, two passes.  phase 0: stats[0] = global count and stats[1] =
- * global sum must be set (all-reduced across ranks) -> mean, stats[3] = local sum sq dev.
- * phase 1 (after all-reducing stats[3]): stats[4] = unbiased std.
- * phase 2 (one pass, after all-reducing stats[0..3] as dxrl_pg_gae left them): mean,
- * stats[3] = sum sq dev = sum(adv^2) - mean sum(adv), stats[4] = unbiased std. */
+/* Global advantage statistics from every rank's (count, mean, M2) triple -- moments f64
+ * [world][3] in rank order (all-gathered stats[5..7]) -- merged in rank order into
+ * stats[0] count, [1] sum, [2] mean, [3] sum of squared deviations, [4] unbiased std (what the
+ * train passes read: (adv - [2]) / ([4] + 1e-8)). */
+int dxrl_pg_adv_combine(int32_t device, const double* moments, int32_t world, double* stats, void* stream);
+/* One rank: dxrl_pg_adv_combine(stats + 5, world = 1).  phase must be 2; adv / count /
+ * partial are unused (kept for ABI stability). */
 int dxrl_pg_adv_finalize(int32_t device, int32_t phase, const float* adv, int64_t count, double* partial,
                          double* stats, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Curriculum-scheduler feed (config C3; replaces the per-episode
+ * CurriculumScheduler.update() calls of evaluation/component_ablation.py:160-170,
+ * experiments/curriculum_scheduler.py:116-170 for a vectorised iteration).
+ * Walks the rollout's episode-end codes (dxrl_pg_rollout_args.ep_code) of all
+ * ranks in (end step, global env id) order and reports what the host scheduler
+ * needs to replay the batch exactly.
+ * ------------------------------------------------------------------------ */
+#define DXRL_SCHED_MAX_CANDIDATES 64
+typedef struct dxrl_sched_args {
+    const uint16_t* codes;     /* u16 [world][T][N] episode-end codes, rank-major (all-gathered) */
+    int32_t world, horizon;    /* ranks, T                                                 */
+    int64_t num_envs;          /* N per rank                                               */
+    int32_t window;            /* window_size (>= 1)                                       */
+    int32_t max_candidates;    /* P <= DXRL_SCHED_MAX_CANDIDATES progressions still possible */
+    double threshold;          /* success_rate_threshold                                   */
+    int64_t min_episodes;      /* min_episodes_before_progression                          */
+    int64_t episodes_before;   /* total_episodes before this batch (== len(episode_successes)) */
+    const uint16_t* tail_in;   /* u16 [window] codes of the last tail_len_in episodes, oldest first */
+    const int32_t* tail_len_in;   /* i32 [1] (device)                                      */
+    uint16_t* tail_out;        /* u16 [window] the new tail (must not alias tail_in)       */
+    int32_t* tail_len_out;     /* i32 [1] (device)                                         */
+    void* scratch;             /* device scratch of dxrl_sched_scratch_bytes()             */
+    int64_t scratch_bytes;
+    int64_t* summary;          /* i64 [4 + 3 P] (device): [0] episodes, [1] steps, [2] successes,
+                                  [3] candidates found (<= P), then per candidate in episode order:
+                                  episode index k in the batch, steps through k, successes among
+                                  the window ending at k                                        */
+} dxrl_sched_args;
+int dxrl_sched_scratch_bytes(int32_t world, int32_t horizon, int64_t num_envs, int32_t window, int64_t* bytes);
+int dxrl_sched_scan(int32_t device, const dxrl_sched_args* args, void* stream);
 
 typedef struct dxrl_pg_heads_args {
     const float* mu;           /* f32 [M][32] actor head output            */

@@ -23,6 +23,15 @@ promotion:
 * ``oracle_run_episode``  <- training/episode_utils.py:13-55
 * ``oracle_eval_program`` <- evaluation/evaluator.py:71-181, robustness_tests.py:240-310
   (pinned by tests/test_eval_host.py against tests/golden/eval_golden.json)
+
+Throughput-mode RNG (the build's own, not the reference's: the reference draws reset
+values from gymnasium's PCG64, which the device replaces with per-env Philox4x32-10
+streams -- distributional parity only, SURVEY.md §7 "RNG parity"):
+
+* ``philox4x32_10`` / ``env_key`` / ``philox_reset_draws`` restate csrc/dxrl_device.h
+  (philox, env_key, env_reset_philox) so the full-size rollout tests can replay a lane's
+  auto-resets.  Pinned by the Random123 known-answer vectors for philox4x32-10
+  (tests/test_oracle_golden.py::test_philox_known_answers).
 """
 from __future__ import annotations
 
@@ -341,3 +350,53 @@ def oracle_eval_program(curricula, lane_off, segments, reset_tape, policy_tapes,
                         break
                 ret[rec], length[rec], succ[rec], cont[rec], hist[rec] = total, len(h), te, h[-1], h
     return ret, length, succ, cont, hist
+
+
+# ---------------------------------------------------------------- device RNG restatement
+_PH_M0, _PH_M1, _PH_W0, _PH_W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+_STREAM_RESET = 0x52535400  # csrc/dxrl_device.h kStreamReset
+_U32 = 0xFFFFFFFF
+
+
+def philox4x32_10(ctr, key):
+    """Philox4x32-10 (Salmon et al., SC'11; Random123): 10 rounds of the two 32x32->64
+    multiplies, Weyl key bumps (csrc/dxrl_device.h philox)."""
+    x, y, z, w = (int(v) & _U32 for v in ctr)
+    k0, k1 = int(key[0]) & _U32, int(key[1]) & _U32
+    for _ in range(10):
+        p0, p1 = _PH_M0 * x, _PH_M1 * z
+        x, y, z, w = ((p1 >> 32) ^ y ^ k0) & _U32, p1 & _U32, ((p0 >> 32) ^ w ^ k1) & _U32, p0 & _U32
+        k0, k1 = (k0 + _PH_W0) & _U32, (k1 + _PH_W1) & _U32
+    return x, y, z, w
+
+
+def env_key(seed: int, gid: int):
+    """Per-env Philox key from (VecEnv seed, global env id) (csrc/dxrl_device.h env_key)."""
+    seed &= (1 << 64) - 1
+    k0 = ((gid & _U32) ^ (((seed >> 32) * 0x85EBCA6B) & _U32)) & _U32
+    k1 = ((seed & _U32) ^ ((((gid >> 32) & _U32) * 0xC2B2AE35) & _U32)) & _U32
+    return k0, k1
+
+
+def _u01_53(hi, lo):
+    return float(((hi << 32) | lo) >> 11) * (1.0 / 9007199254740992.0)
+
+
+def philox_reset_draws(cur: OracleCurriculum, k0: int, k1: int, ctr: int) -> np.ndarray:
+    """The 21 reset slots of a device-RNG reset with counter ``ctr`` (csrc/dxrl_device.h
+    env_reset_philox): slot k is the 53-bit uniform of Philox block k // 2 (half k % 2);
+    jp = -0.1 + 0.2 u, size / mass / friction / spawn = lo + (hi - lo) u (the reference's
+    uniform(low, high) form, experiments/config.py:44-113); NaN where the curriculum has no
+    range (the constant is used)."""
+    u = []
+    for b in range((D + 6 + 1) // 2):
+        r = philox4x32_10((ctr & _U32, (ctr >> 32) & _U32, _STREAM_RESET, b), (k0, k1))
+        u += [_u01_53(r[0], r[1]), _u01_53(r[2], r[3])]
+    d = np.empty(D + 6)
+    for k in range(D):
+        d[k] = -0.1 + (0.1 - -0.1) * u[k]
+    rngs = (cur.size_range, cur.mass_range, cur.friction_range, cur.spawn_x_range, cur.spawn_y_range,
+            cur.spawn_z_range)
+    for k, rg in enumerate(rngs):
+        d[D + k] = math.nan if rg is None else rg[0] + (rg[1] - rg[0]) * u[D + k]
+    return d

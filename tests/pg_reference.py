@@ -68,13 +68,16 @@ def gae(rew, done, V, n, T, gamma, lam):
 
 
 def loss_and_grads(params, obs_rm, act, logp_old, rew, done, n, T, cfg, bf16=True, norm_stats=None, total=None,
-                   world=1):
+                   world=1, scales=None):
     """Manual forward/backward of the PPO objective as the HIP pipeline computes it.
     Sharded use (as PGTrainer with world > 1): norm_stats(adv) -> (mean, std) computed
-    across ranks, total = global sample count, world = number of ranks.
+    across ranks, total = global sample count, world = number of ranks; or
+    scales = (per-sample loss scale, per-rank entropy coefficient) as
+    distributed.loss_scales returns them (what the trainer hands the kernels).
     Returns (grads [NPARAMS], info dict)."""
     M = n * T
     total = M if total is None else total
+    inv_total, ent = (1.0 / total, cfg["ent_coef"] / world) if scales is None else scales
     Wd = unpack(params)
     dt = params.dtype
     X = obs_rm.to(dt)
@@ -97,11 +100,11 @@ def loss_and_grads(params, obs_rm, act, logp_old, rew, done, n, T, cfg, bf16=Tru
     ratio = torch.exp(lp - logp_old)
     s1, s2 = ratio * A, torch.clamp(ratio, 1 - cfg["clip_eps"], 1 + cfg["clip_eps"]) * A
     rc = torch.clamp(ratio, 1 - cfg["clip_eps"], 1 + cfg["clip_eps"])
-    gsel = torch.where((s1 <= s2) | (ratio == rc), -A * ratio, torch.zeros_like(A)) / total
+    gsel = torch.where((s1 <= s2) | (ratio == rc), -A * ratio, torch.zeros_like(A)) * inv_total
     d = a - mu
     dmu = gsel[:, None] * d * iv
-    dls = (gsel[:, None] * (d * d * iv - 1.0)).sum(0) - cfg["ent_coef"] / world
-    dv = 2.0 * cfg["vf_coef"] * (V[:M] - ret) / total
+    dls = (gsel[:, None] * (d * d * iv - 1.0)).sum(0) - ent
+    dv = 2.0 * cfg["vf_coef"] * (V[:M] - ret) * inv_total
     grads = torch.zeros(NPARAMS, dtype=dt, device=params.device)
     G = unpack(grads)
     G["logstd"].copy_(dls)

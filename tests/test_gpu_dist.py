@@ -1,0 +1,66 @@
+"""GPU, multi-rank: PGTrainer sharded over two ranks (two processes on cuda:0, gloo
+process group -- RCCL needs one GPU per rank, which a one-GPU test box does not
+have) equals the world-1 trainer on the concatenated batch ("the
+8-rank loss/params must equal 1-rank on the concatenated batch within fp32
+reduction-order tolerance").  Same global env ids -> bit-identical rollout tapes;
+the gradient SUM and the advantage moments differ from world 1 only in
+summation order."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(tmp, world, n, iters, config):
+    port = _port()
+    procs, outs = [], []
+    for r in range(world):
+        out = os.path.join(tmp, f"w{world}_r{r}.pt")
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_pg_worker.py"), out, str(n),
+                                       str(iters), config], env=env))
+        outs.append(out)
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    return [torch.load(o, weights_only=False) for o in outs]
+
+
+@pytest.mark.parametrize("config", ["variable", "default"])
+def test_two_ranks_equal_one_rank_on_concatenated_batch(tmp_path, config):
+    n, iters = 256, 3
+    one = _launch(str(tmp_path), 1, 2 * n, iters, config)[0]
+    two = _launch(str(tmp_path), 2, n, iters, config)
+    # the first iteration's tapes: rank r holds env columns [r n, (r+1) n) of the world-1 run
+    for r, res in enumerate(two):
+        assert torch.equal(res["rew0"], one["rew0"][:, r * n:(r + 1) * n])
+        assert torch.equal(res["done0"], one["done0"][:, r * n:(r + 1) * n])
+    # every rank ends with the same parameters (identical Adam inputs after the all-reduce)
+    assert torch.equal(two[0]["params"], two[1]["params"])
+    # global advantage moments and normalisation == world 1 (f64, summation order only)
+    for k in (0, 1, 2, 4):
+        a, b = two[0]["stats0"][k].item(), one["stats0"][k].item()
+        assert abs(a - b) <= 1e-9 * max(1.0, abs(b)), (k, a, b)
+    # the first iteration's all-reduced gradient == the world-1 gradient (f32 summation order)
+    g2, g1 = two[0]["grads0"], one["grads0"]
+    rel = (g2 - g1).norm() / g1.norm()
+    assert rel < 1e-4, rel.item()
+    # after `iters` Adam steps the parameters still agree to f32 reduction-order tolerance
+    p2, p1 = two[0]["params"], one["params"]
+    assert (p2 - p1).abs().max().item() < 1e-4 * max(1.0, p1.abs().max().item())
+    if config == "default":
+        assert two[0]["sched"] == two[1]["sched"] == one["sched"]

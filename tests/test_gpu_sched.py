@@ -1,0 +1,102 @@
+"""GPU: the curriculum-scheduler feed (csrc/dxrl_sched.hip, config C3).
+
+dxrl_sched_scan against its NumPy restatement (tests/sched_reference.py, itself
+checked against one CurriculumScheduler.update() per episode in
+tests/test_host_logic.py) on random multi-rank episode-end code tapes, and
+PGTrainer's device feed against its host feed (codes copied back, update_batch)
+over several training iterations."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+import sched_reference as SR
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def N():
+    import dexterous_rl_manipulation_amd  # noqa: F401
+    from dexterous_rl_manipulation_amd import _native
+    return _native
+
+
+def _scan(N, codes, window, thr, min_ep, before, P, tail):
+    world, T, n = codes.shape
+    dev = torch.device("cuda", 0)
+    c = torch.from_numpy(codes.astype(np.uint16).view(np.int16)).to(dev)
+    tail_in = torch.zeros(window, dtype=torch.int16, device=dev)
+    tail_in[:len(tail)] = torch.tensor(np.asarray(tail, dtype=np.int64).astype(np.uint16).view(np.int16))
+    tail_out = torch.full((window,), -1, dtype=torch.int16, device=dev)
+    tl = torch.tensor([len(tail), -1], dtype=torch.int32, device=dev)
+    nb = C.c_int64()
+    N.call("dxrl_sched_scratch_bytes", world, T, n, window, C.byref(nb))
+    scratch = torch.empty(nb.value, dtype=torch.uint8, device=dev)
+    summary = torch.full((4 + 3 * N.SCHED_MAX_CANDIDATES,), -7, dtype=torch.int64, device=dev)
+    a = N.SchedArgs()
+    a.codes, a.world, a.horizon, a.num_envs = N.ptr(c), world, T, n
+    a.window, a.max_candidates, a.threshold, a.min_episodes, a.episodes_before = window, P, thr, min_ep, before
+    a.tail_in, a.tail_len_in, a.tail_out, a.tail_len_out = N.ptr(tail_in), N.ptr(tl[0:1]), N.ptr(tail_out), \
+        N.ptr(tl[1:2])
+    a.scratch, a.scratch_bytes, a.summary = N.ptr(scratch), nb.value, N.ptr(summary)
+    N.call("dxrl_sched_scan", 0, C.byref(a), N.stream_of(dev))
+    torch.cuda.synchronize()
+    s = summary.cpu().numpy()
+    nl = int(tl[1].item())
+    return s, tail_out.cpu().numpy().view(np.uint16)[:nl].astype(np.int64)
+
+
+@pytest.mark.parametrize("world,T,n", [(1, 7, 5), (2, 13, 33), (3, 4, 100), (1, 200, 4096), (2, 200, 4096),
+                                       (8, 20, 1000)])
+def test_scan_matches_restatement(N, world, T, n):
+    rng = np.random.default_rng(world * 1000 + T + n)
+    for trial in range(6):
+        p_end, p_succ = rng.random(), rng.random()
+        lens = rng.integers(1, 16383, (world, T, n))
+        codes = np.where(rng.random((world, T, n)) < p_end, (lens << 1) | (rng.random((world, T, n)) < p_succ), 0)
+        window = int(rng.choice([1, 2, 15, 20, 64, 1000]))
+        thr = float(rng.choice([0.0, 0.3, 0.5, 0.9, 1.0]))
+        min_ep, before = int(rng.integers(0, 50)), int(rng.integers(0, 3000))
+        P = int(rng.integers(0, N.SCHED_MAX_CANDIDATES + 1))
+        tail = (rng.random(min(window, before)) < p_succ).astype(np.int64)
+        s, new_tail = _scan(N, codes, window, thr, min_ep, before, P, tail)
+        r = SR.scan(codes, window, thr, min_ep, before, P, tail)
+        assert (s[0], s[1], s[2]) == (r["episodes"], r["steps"], r["successes"]), trial
+        found = int(s[3])
+        assert found == len(r["candidates"]), trial
+        assert [tuple(int(x) for x in s[4 + 3 * j:7 + 3 * j]) for j in range(found)] == r["candidates"], trial
+        assert np.array_equal(new_tail, r["tail"]), trial
+
+
+def test_scan_empty_batch(N):
+    codes = np.zeros((2, 5, 9), dtype=np.int64)
+    s, tail = _scan(N, codes, 4, 0.5, 0, 10, 3, [1, 0, 1, 1])
+    assert list(s[:4]) == [0, 0, 0, 0] and list(tail) == [1, 0, 1, 1]
+
+
+@pytest.mark.parametrize("threshold", [0.3, 0.6])
+def test_trainer_device_feed_equals_host_feed(threshold):
+    """PGTrainer with a history="window" scheduler (device scan, only the summary crosses PCIe)
+    and a history="full" twin (codes copied back, update_batch) progress at the same
+    episodes with the same totals, statistics and history entries, iteration by iteration."""
+    import dexterous_rl_manipulation_amd as pkg
+    C_ = pkg.CurriculumConfig
+    runs = []
+    for history in ("window", "full"):
+        env = pkg.envs.VecEnv(256, curriculum_config=C_.easy(), reward_type="dense", seed=5)
+        tr = pkg.trainer.PGTrainer(env, pkg.trainer.TrainerConfig(horizon=32, seed=2, max_steps=9))
+        sc = pkg.experiments.CurriculumScheduler(C_.easy(), C_.hard(), threshold, 500, 15, 4, history=history)
+        tr.attach_curriculum(sc)
+        env.reset(write_obs=False)
+        stats = []
+        for _ in range(6):
+            tr.iteration()
+            torch.cuda.synchronize()
+            stats.append((sc.get_statistics(), float(env.curriculum_configs[0].object_size), tr._sched_mode))
+        runs.append(stats)
+    for (a, sa, ma), (b, sb, mb) in zip(*runs):
+        assert ma == "device" and mb == "host"
+        assert a == b and sa == sb
+    assert runs[0][-1][0]["num_progressions"] > 0

@@ -166,3 +166,87 @@ def test_scheduler_update_batch_equals_sequential_updates():
             assert type(b.total_episodes) is int and type(b.total_steps) is int
             assert a.current_difficulty_level == b.current_difficulty_level
             assert a.progression_history == b.progression_history and a.current_config == b.current_config
+
+
+def _sched_kw(rng):
+    return dict(success_rate_threshold=float(rng.choice([0.0, 0.3, 0.5, 0.7])),
+                min_episodes_before_progression=int(rng.integers(0, 40)), window_size=int(rng.integers(1, 25)),
+                progression_steps=int(rng.integers(1, 7)))
+
+
+def test_step_based_update_batch_equals_sequential_updates():
+    """StepBasedScheduler.update_batch == one update() per episode: a milestone fires at the
+    first episode whose running step total reaches it, at most one per episode
+    (curriculum_scheduler.py:276-335)."""
+    from dexterous_rl_manipulation_amd.experiments import CurriculumConfig as CC, StepBasedScheduler
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        ms = sorted(rng.integers(0, 3000, int(rng.integers(1, 6))).tolist())
+        a = StepBasedScheduler(CC.easy(), CC.hard(), ms, **_sched_kw(rng))
+        b = StepBasedScheduler(CC.easy(), CC.hard(), ms, **_sched_kw(rng))
+        b.__dict__.update({k: v for k, v in a.__dict__.items() if not isinstance(v, list)})
+        for _ in range(int(rng.integers(1, 6))):
+            m = int(rng.integers(0, 40))
+            s, st = rng.random(m) < 0.5, rng.integers(1, 200, m)
+            assert any([a.update(bool(x), int(y)) for x, y in zip(s, st)]) == b.update_batch(s, st)
+            assert a.episode_successes == b.episode_successes and a.episode_steps == b.episode_steps
+            assert (a.total_steps, a.total_episodes, a.current_milestone_idx) == \
+                (b.total_steps, b.total_episodes, b.current_milestone_idx)
+            assert a.progression_history == b.progression_history and a.current_config == b.current_config
+
+
+def test_window_history_matches_full_history():
+    """history="window" keeps the last window_size episodes and counters only: totals,
+    statistics and progression history equal the full-history scheduler's."""
+    from dexterous_rl_manipulation_amd.experiments import CurriculumConfig as CC, CurriculumScheduler
+    rng = np.random.default_rng(2)
+    for _ in range(100):
+        kw = _sched_kw(rng)
+        a = CurriculumScheduler(CC.easy(), CC.hard(), **kw)
+        b = CurriculumScheduler(CC.easy(), CC.hard(), history="window", **kw)
+        for _ in range(int(rng.integers(1, 6))):
+            m = int(rng.integers(0, 60))
+            s, st = rng.random(m) < rng.random(), rng.integers(1, 200, m)
+            if rng.random() < 0.5:
+                assert a.update_batch(s, st) == b.update_batch(s, st)
+            else:
+                assert any([a.update(bool(x), int(y)) for x, y in zip(s, st)]) == \
+                    any([b.update(bool(x), int(y)) for x, y in zip(s, st)])
+            assert a.get_statistics() == b.get_statistics()
+            assert b.episode_successes == a.episode_successes[-kw["window_size"]:]
+            assert len(b.episode_steps) <= kw["window_size"]
+
+
+@pytest.mark.parametrize("history", ["window", "full"])
+def test_device_summary_replay_equals_sequential_updates(history):
+    """The dxrl_sched_scan contract (restated in tests/sched_reference.py) replayed by
+    CurriculumScheduler.apply_device_summary == one update() per episode in (end step,
+    global env id) order, over random multi-rank code tapes and several batches."""
+    import sched_reference as SR
+    from dexterous_rl_manipulation_amd.experiments import CurriculumConfig as CC, CurriculumScheduler
+    rng = np.random.default_rng(3)
+    for _ in range(150):
+        kw = _sched_kw(rng)
+        a = CurriculumScheduler(CC.easy(), CC.hard(), **kw)
+        b = CurriculumScheduler(CC.easy(), CC.hard(), history=history, **kw)
+        w = kw["window_size"]
+        for _ in range(int(rng.integers(1, 5))):
+            world, T, n = int(rng.integers(1, 4)), int(rng.integers(1, 9)), int(rng.integers(1, 12))
+            p_end, p_succ = rng.random(), rng.random()
+            lens = rng.integers(1, 300, (world, T, n))
+            codes = np.where(rng.random((world, T, n)) < p_end, (lens << 1) | (rng.random((world, T, n)) < p_succ), 0)
+            ep = SR.order_codes(codes)
+            want = any([a.update(bool(c & 1), int(c >> 1)) for c in ep])
+            P = b.remaining_progressions(64)
+            tail_in = [int(x) for x in b.episode_successes[-w:]]
+            r = SR.scan(codes, w, kw["success_rate_threshold"], kw["min_episodes_before_progression"],
+                        b.total_episodes, P, tail_in)
+            got = b.apply_device_summary(r["episodes"], r["steps"], r["successes"], r["candidates"],
+                                         r["tail"][len(r["tail"]) - min(w, len(ep)):],
+                                         episode_codes=ep if history == "full" else None)
+            assert want == got
+            assert a.get_statistics() == b.get_statistics()
+            assert b.episode_successes == a.episode_successes[-len(b.episode_successes):]
+            assert b.episode_steps == a.episode_steps[-len(b.episode_steps):]
+            if history == "full":
+                assert a.episode_successes == b.episode_successes and a.episode_steps == b.episode_steps

@@ -124,3 +124,15 @@ def test_noise_wrapper(ci):
                 obs = oracle_noisy_obs(obs, nrng.normal(0, c["obs_std"], size=45))
             assert np.array_equal(obs, z["obs"][e, t]), (e, t)
             assert math.isclose(r, z["reward"][e, t], rel_tol=1e-12, abs_tol=1e-15)
+
+
+def test_philox_known_answers():
+    """The oracle's Philox4x32-10 (restating csrc/dxrl_device.h) against the Random123
+    known-answer vectors (kat_vectors, philox4x32 10)."""
+    from oracle.dx_oracle import philox4x32_10
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, want in kat:
+        assert philox4x32_10(ctr, key) == want

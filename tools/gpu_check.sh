@@ -20,7 +20,7 @@ run() {  # name timeout cmd...
 STEPS=${STEPS:-pytest smoke bench prof}
 for s in $STEPS; do
   case $s in
-    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     configs) for c in default hard_heldout variable_noise; do

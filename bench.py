@@ -43,6 +43,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# oracle loop / the reference's own loop, same core, build container (tools/cpu_ratio.py)
+RESTATEMENT_SPEED_RATIO = {"easy": 1.26, "hard": 0.96}
 STEP_BYTES_PER_ENV = 594  # k_step algorithmic bytes per env-step
 
 
@@ -218,12 +220,12 @@ def rollout_bench(args, world, rank, dev):
     return wall, kernel_ms
 
 
-def step_kernel_roofline(args, dev):
-    """k_step at large N: algorithmic bytes / HIP-event time per launch."""
+def step_kernel_time(n, launches, dev, seed=5):
+    """k_step (dxrl_env_step) on n envs: HIP events around `launches` back-to-back launches on
+    the launch stream; ms per launch (synthetic U(-1.2, 1.2) actions, variable curriculum)."""
     from dexterous_rl_manipulation_amd import envs
     import dexterous_rl_manipulation_amd as pkg
-    n = args.roofline_envs
-    env = envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.variable(), reward_type="dense", seed=5,
+    env = envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.variable(), reward_type="dense", seed=seed,
                       device=dev)
     env.reset(write_obs=False)
     gen = torch.Generator(device=dev)
@@ -235,11 +237,29 @@ def step_kernel_roofline(args, dev):
     stream = torch.cuda.current_stream(dev)  # dxrl_env_step launches on this stream
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
-    for _ in range(args.roofline_launches):
+    for _ in range(launches):
         env.step(acts)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    ms = ev0.elapsed_time(ev1) / args.roofline_launches  # back-to-back launches, average per launch
+    ms = ev0.elapsed_time(ev1) / launches
+    del env, acts
+    torch.cuda.empty_cache()
+    return ms
+
+
+def step_kernel_small(n, dev):
+    """The BASELINE.md "step-kernel env-steps/s @4096" column: k_step at the bench's env count
+    (cache-resident, launch-latency bound; not a roofline figure)."""
+    ms = step_kernel_time(n, 200, dev)
+    return {"envs": n, "us_per_launch": round(ms * 1e3, 2), "env_steps_per_s": round(n / (ms * 1e-3), 1),
+            "algorithmic_GB_s": round(STEP_BYTES_PER_ENV * n / (ms * 1e-3) / 1e9, 1),
+            "note": "back-to-back launches, HIP events; working set in L2 / Infinity Cache"}
+
+
+def step_kernel_roofline(args, dev):
+    """k_step at large N: algorithmic bytes / HIP-event time per launch."""
+    n = args.roofline_envs
+    ms = step_kernel_time(n, args.roofline_launches, dev)
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
     if os.path.exists(pmc):
@@ -249,28 +269,26 @@ def step_kernel_roofline(args, dev):
             traffic = d.get("hbm_bytes_per_launch")
     bytes_per_launch = STEP_BYTES_PER_ENV * n
     achieved = bytes_per_launch / (ms * 1e-3) / 1e9
-    del env, acts
-    torch.cuda.empty_cache()
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "kernel": "k_step (dxrl_env_step)",
             "envs": n, "bytes_per_env_step": STEP_BYTES_PER_ENV, "ms_per_launch": round(ms, 4),
             "env_steps_per_s": round(n / (ms * 1e-3), 1)}
 
 
-def cpu_baseline(args):
-    """The reference algorithm restated (oracle/dx_oracle.py) in the reference's
-    own loop shape: run_episode + SimpleLearner, one env, one core."""
+def _cpu_worker(curriculum, seconds, seed, out):
+    """One host core: the reference's run_episode + SimpleLearner loop over the oracle env
+    (training/episode_utils.py:13-55, policies/simple_learner.py:49-99), 1 env."""
     from oracle.dx_oracle import OracleCurriculum, OracleEnv, OracleSimpleLearner, reset_draws
     presets = {"easy": dict(object_size=0.08, object_mass=0.05, friction_coefficient=0.8),
-               "medium": {}, "hard": dict(object_size=0.03, object_mass=0.2, friction_coefficient=0.3)}
-    cur = OracleCurriculum(**presets.get(args.curriculum, {}))
+               "medium": {}, "hard": dict(object_size=0.03, object_mass=0.2, friction_coefficient=0.3),
+               "variable": dict(size_range=(0.03, 0.07), mass_range=(0.05, 0.15), friction_range=(0.3, 0.7))}
+    cur = OracleCurriculum(**presets.get(curriculum, {}))
     env = OracleEnv(cur=cur, dense=True)
-    pol = OracleSimpleLearner(np.random.RandomState(42).standard_normal(4_000_000), learning_rate=0.01)
-    rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence(1000)))
-    steps = 0
-    first = True
+    pol = OracleSimpleLearner(np.random.RandomState(42 + seed).standard_normal(4_000_000), learning_rate=0.01)
+    rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence(1000 + seed)))
+    steps, first = 0, True
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < args.cpu_seconds and pol.cur < 3_900_000:
+    while time.perf_counter() - t0 < seconds and pol.cur < 3_900_000:
         env.reset(reset_draws(rng, cur, first))
         first = False
         pol.reset()
@@ -281,16 +299,61 @@ def cpu_baseline(args):
             steps += 1
             if te or tr:
                 break
-    dt = time.perf_counter() - t0
-    return {"value": round(steps / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/dx_oracle.py run_episode+SimpleLearner loop, config_{args.curriculum}, 1 env, "
-                      f"{steps} env-steps in {dt:.1f} s on 1 host core"}
+    out.put((steps, time.perf_counter() - t0))
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(args):
+    """The reference algorithm restated (oracle/dx_oracle.py) in the reference's own loop shape,
+    1 env per process: P = 1 and P = every host core this job may use (the
+    affinity mask, at most 16 -- the box's CPU share per GPU), `--cpu-seconds` each.  Runs
+    before this process touches the GPU; workers are spawned interpreters."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    p_all = max(1, min(avail, 16))
+    res = {}
+    for P in sorted({1, p_all}):
+        q = ctx.Queue()
+        procs = [ctx.Process(target=_cpu_worker, args=(args.curriculum, args.cpu_seconds, k, q)) for k in range(P)]
+        for pr in procs:
+            pr.start()
+        got = [q.get(timeout=args.cpu_seconds + 120) for _ in procs]
+        for pr in procs:
+            pr.join()
+        res[P] = (sum(st for st, _ in got), sum(st / dt for st, dt in got))
+    steps1, v1 = res[1]
+    stepsP, vP = res[p_all]
+    return {"value": round(vP, 1), "unit": "env-steps/s", "cores": p_all, "kind": "port",
+            "single_core": round(v1, 1), "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": f"oracle/dx_oracle.py run_episode+SimpleLearner loop (the reference's loop restated), "
+                      f"config_{args.curriculum}, 1 env per process, {args.cpu_seconds:.0f} s per run: "
+                      f"P=1 {steps1} env-steps, P={p_all} {stepsP} env-steps (aggregate of per-process rates); "
+                      f"the restatement runs at {RESTATEMENT_SPEED_RATIO} x the reference's own loop speed on one "
+                      f"core (tools/cpu_ratio.py, DESIGN.md §6)"}
 
 
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
+    cpu = None
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)  # before the GPU is touched (spawned workers)
     world, rank, local = dist_setup(args)
     dev = torch.device("cuda", local if world > 1 else 0)
     total_steps = args.envs * world * args.horizon * args.steps
@@ -325,8 +388,9 @@ def main():
     out.update(extra)
     if rank == 0 and not args.no_roofline:
         out["roofline"] = step_kernel_roofline(args, dev)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args)
+        out["step_kernel_at_bench_envs"] = step_kernel_small(args.envs, dev)
+    if rank == 0 and cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

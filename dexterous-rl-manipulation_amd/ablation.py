@@ -105,6 +105,13 @@ def train_many(jobs: Sequence[Tuple[AblationConfig, int]], num_episodes: int = 2
                chunk_steps: int = 2048) -> Tuple[List[TrainingResults], List[int]]:
     """Every (configuration, seed) job as one env lane of fused rollouts (one env handle per
     reward type); returns the results in job order and the gauss draws each learner consumed."""
+    if (curriculum_scheduler_config is not None and curriculum_scheduler_config.success_rate_threshold <= 0
+            and any(c.use_curriculum for c, _ in jobs)):
+        # with threshold <= 0 the reference's scheduler progresses even though training
+        # episodes never report success (mean of an all-False window is 0.0 >= threshold,
+        # component_ablation.py:160-170); the lanes here keep the initial difficulty
+        raise ValueError("train_many assumes the ablation scheduler never progresses; "
+                         "success_rate_threshold must be > 0")
     env_seeds = list(env_seeds) if env_seeds is not None else [None] * len(jobs)
     env_seeds = [_entropy_seed() if s is None else int(s) for s in env_seeds]
     results: List[Optional[TrainingResults]] = [None] * len(jobs)

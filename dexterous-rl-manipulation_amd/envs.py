@@ -308,6 +308,7 @@ class DexterousManipulationEnv(_EnvBase):
     """Drop-in for envs/manipulation_env.py:14-349 backed by the HIP kernels."""
 
     metadata = {"render_modes": ["human", "rgb_array"], "render_fps": 30}
+    _warned_f64 = False
 
     def __init__(self, num_fingers: int = 5, joints_per_finger: int = 3,
                  object_position: Optional[np.ndarray] = None, max_episode_steps: int = 200,
@@ -379,7 +380,19 @@ class DexterousManipulationEnv(_EnvBase):
         return obs, self._info(op.astype(np.float32), obs)
 
     def step(self, action: np.ndarray):
-        a = np.asarray(action, dtype=np.float32).reshape(1, self.num_joints)
+        raw = np.asarray(action)
+        if raw.dtype == np.float64 and not DexterousManipulationEnv._warned_f64:
+            # NEP 50: the reference's `0.9 * jv + 0.1 * action` turns a float64 action into
+            # float64 joint velocities (and positions) for the rest of the episode
+            # (manipulation_env.py:203-205); the device state stays float32, so bit parity
+            # holds for float32 actions (what Box.sample, SimpleLearner and the bundled
+            # policies return).
+            import warnings
+            warnings.warn("DexterousManipulationEnv.step: float64 action cast to float32 (the reference would "
+                          "carry float64 joint state; parity is defined for float32 actions)", RuntimeWarning,
+                          stacklevel=2)
+            DexterousManipulationEnv._warned_f64 = True
+        a = raw.astype(np.float32, copy=False).reshape(1, self.num_joints)
         self._act.copy_(torch.from_numpy(a))
         self._vec.step(self._act, components=True)
         obs, op, reward, comps, term, trunc = self._fetch(with_step=True)

@@ -71,7 +71,9 @@ class ReferenceStreams:
         self.rngs = [np.random.Generator(np.random.PCG64(np.random.SeedSequence(int(s)))) for s in env_seeds]
         self.legacy = [np.random.RandomState(int(s)) for s in learner_seeds]
         self.gbuf: List[np.ndarray] = [np.empty(0) for _ in env_seeds]
-        self.first = [True] * env.num_envs
+        # the first reset draws the spawn position only when the env was built without
+        # object_position (manipulation_env.py:156-161)
+        self.first = [not bool(env._cfg.has_object_position)] * env.num_envs
 
     def curriculum_of(self, i: int, env_index: Optional[np.ndarray]):
         row = 0 if env_index is None else int(env_index[i])

@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's)")
     p.add_argument("--horizon", type=int, default=200, help="env steps per bench step (rollout length)")
     p.add_argument("--curriculum", default=None, help="override the config's curriculum preset")
+    p.add_argument("--epochs", type=int, default=1, help="PPO epochs per iteration (default 1: A2C-style step)")
+    p.add_argument("--minibatches", type=int, default=1, help="PPO minibatches per epoch")
     p.add_argument("--learner", choices=["pg", "simple"], default="pg",
                    help="pg: MLP actor-critic policy-gradient iteration (default); simple: SimpleLearner rollout")
     p.add_argument("--roofline-envs", type=int, default=1 << 22)
@@ -147,7 +149,8 @@ def pg_bench(args, world, rank, dev):
         import torch.distributed as dist
         pg = dist.group.WORLD
     env, tr = build_pg_workload(args.config, dev, rank=rank, world=world, process_group=pg, envs=args.envs,
-                                horizon=args.horizon, curriculum=args.curriculum)
+                                horizon=args.horizon, curriculum=args.curriculum, epochs=args.epochs,
+                                minibatches=args.minibatches)
     for _ in range(args.warmup):
         tr.iteration()
     torch.cuda.synchronize(dev)
@@ -173,7 +176,7 @@ def pg_bench(args, world, rank, dev):
     M = tr.M
     gemm_ms = sum(v for k, v in phases.items() if k not in ("rollout", "advantages", "optimizer_step",
                                                             "schedule_feed", "schedule_apply"))
-    train_flops = M * (FWD_BOTH + BWD_BOTH)
+    train_flops = M * args.epochs * (FWD_BOTH + BWD_BOTH)
     mfma = {"bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_BF16_TFS,
             "training_gemms_achieved": round(train_flops / (gemm_ms * 1e-3) / 1e12, 2),
             "rollout_policy_achieved": round(M * FWD_ACTOR / (phases["rollout"] * 1e-3) / 1e12, 2),
@@ -360,9 +363,11 @@ def main():
     extra = {}
     if args.learner == "pg":
         wall, phases, mfma, stats = pg_bench(args, world, rank, dev)
+        upd = ("1 epoch x 1 minibatch: ratio == 1, an A2C-style step" if args.epochs * args.minibatches == 1
+               else f"{args.epochs} epochs x {args.minibatches} minibatches, one Adam step each")
         workload = (f"{WORKLOADS[args.config]['desc']} PG iteration: fused actor-MLP(256,256) rollout of "
-                    f"{args.horizon} env steps x {args.envs} envs + critic fwd + GAE + adv-norm + PPO heads + "
-                    f"backward + Adam")
+                    f"{args.horizon} env steps x {args.envs} envs + critic fwd + GAE + adv-norm + PPO-clip / value "
+                    f"heads + backward + Adam ({upd})")
         dtype = "bf16 MFMA (f32 acc) + f32/f64 env"
         par = (f"dp{world} (env shards; RCCL all-reduce of the f64 advantage moments and the f32 grads)"
                if world > 1 else "dp1")

@@ -77,6 +77,9 @@ class TrainerConfig:
     fused: bool = True                       # one-pass learner kernels (dxrl_pg_fused) vs the GEMM chain
     h1_recompute: bool = True                # fused dW2: recompute H1 from obs on chip (no H1 HBM round trip)
     record_cap: int = 0                      # per-env episode records per iteration (0 = off)
+    epochs: int = 1                          # PPO epochs over the iteration's samples
+    minibatches: int = 1                     # time-contiguous minibatches per epoch, order shuffled per epoch
+                                             # (1 x 1: one update, ratio == 1 -- an A2C-style step)
     success_rule: str = "terminated"         # "training" (episode_utils.py:52) or "terminated"
 
 
@@ -95,6 +98,12 @@ class PGTrainer:
         if self.M % 32:
             raise ValueError("num_envs * horizon must be a multiple of 32")
         self.max_steps = cfg.max_steps or env.max_episode_steps
+        if cfg.epochs < 1 or cfg.minibatches < 1 or self.M % cfg.minibatches or (self.M // cfg.minibatches) % 32:
+            raise ValueError("epochs >= 1; num_envs * horizon must split into `minibatches` slices of a multiple "
+                             "of 32 samples")
+        if (cfg.epochs > 1 or cfg.minibatches > 1) and not cfg.fused:
+            raise ValueError("epochs / minibatches need the fused learner")
+        self._mb = (0, self.M)  # (first sample, samples) of the minibatch the train passes read
         self.pg = process_group
         self.world = world_size
         self.global_M = global_count(self.M, self.world, self.pg)  # samples of all ranks per iteration
@@ -231,13 +240,17 @@ class PGTrainer:
         self._mlp_forward("a", self.M, self.H1a, self.H2a, head_f32=self.mu)
 
     # ------------------------------------------------------------------ fused path
-    def _fused_args(self, net, train, rows):
+    def _fused_args(self, net, train, rows, start=0):
         c, p = self.cfg, N.ptr
         f = N.PgFusedArgs()
         f.net, f.train, f.rows = net, int(train), rows
-        f.packed, f.params, f.obs = p(self.packed), p(self.params), p(self.obs_rm)
-        f.act, f.logp_old, f.adv, f.ret, f.stats = p(self.act), p(self.logp), p(self.adv), p(self.ret), p(self.stats)
-        f.inv_total_samples, f.ent_coef = loss_scales(self.global_M, self.world, c.ent_coef)
+        f.packed, f.params, f.obs = p(self.packed), p(self.params), p(self.obs_rm[start:])
+        f.act, f.logp_old, f.adv, f.ret = p(self.act[start:]), p(self.logp[start:]), p(self.adv[start:]), \
+            p(self.ret[start:])
+        f.stats = p(self.stats)
+        # each minibatch is one gradient step on the mean loss over its samples of all ranks
+        f.inv_total_samples, f.ent_coef = loss_scales(self.global_M // self.cfg.minibatches, self.world,
+                                                      c.ent_coef)
         f.clip_eps, f.vf_coef = c.clip_eps, c.vf_coef
         f.values = p(self.V[0])
         f.h1, f.dh2 = p(self.H1a), p(self.dH2)
@@ -251,14 +264,33 @@ class PGTrainer:
         N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(1, False, self.M + self.n)), self._s())
 
     def actor_train(self):
-        N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(0, True, self.M)), self._s())
+        start, rows = self._mb
+        N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(0, True, rows, start)), self._s())
 
     def critic_train(self):
-        N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(1, True, self.M)), self._s())
+        start, rows = self._mb
+        N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(1, True, rows, start)), self._s())
+
+    def ppo_updates(self):
+        """epochs x minibatches PPO-clip updates (actor + critic pass and an Adam step each)
+        over time-contiguous slices of the iteration's samples; the slice order is a fresh
+        permutation per epoch (seeded by cfg.seed and the iteration)."""
+        c = self.cfg
+        size = self.M // c.minibatches
+        rng = np.random.default_rng([int(c.seed), self.iteration_index])
+        for _ in range(c.epochs):
+            for k in rng.permutation(c.minibatches):
+                self._mb = (int(k) * size, size)
+                self.actor_train()
+                self.critic_train()
+                self.optimizer_step()
+        self._mb = (0, self.M)
 
     def phases(self):
         """The iteration's launch groups in order (bench.py times each)."""
-        if self.cfg.fused:
+        if self.cfg.fused and self.cfg.epochs * self.cfg.minibatches > 1:
+            ph = ["rollout", "critic_values", "advantages", "ppo_updates"]
+        elif self.cfg.fused:
             ph = ["rollout", "critic_values", "advantages", "actor_train", "critic_train", "optimizer_step"]
         else:
             ph = ["rollout", "critic_forward", "advantages", "actor_forward", "heads", "backward", "optimizer_step"]
@@ -417,7 +449,10 @@ class PGTrainer:
 
     def iteration(self, update: bool = True):
         for name in self.phases():
-            if name != "optimizer_step" or update:
+            if name == "ppo_updates" and not update:
+                self.actor_train()
+                self.critic_train()
+            elif name != "optimizer_step" or update:
                 getattr(self, name)()
         self.iteration_index += 1
 
@@ -432,6 +467,8 @@ class PGTrainer:
         return out
 
     def loss_stats(self) -> Dict[str, float]:
-        s = (self.fused_loss if self.cfg.fused else self.loss_partial).sum(0).cpu().numpy() / self.M
+        """Loss terms of the last train pass (the last minibatch of the last epoch)."""
+        rows = self.M // self.cfg.minibatches
+        s = (self.fused_loss if self.cfg.fused else self.loss_partial).sum(0).cpu().numpy() / rows
         return {"policy_loss": float(s[0]), "value_mse": float(s[1]), "clip_frac": float(s[2]),
                 "approx_kl": float(s[3]), "grad_norm": float(np.sqrt(self.gnorm2.item()))}

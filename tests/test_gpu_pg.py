@@ -321,3 +321,42 @@ def test_lane_split_rollout_matches_64_env_kernel(pkg, cur, n, noise):
                                           env.step_count, env.object_size, env.friction_coefficient)])
     for k, (a, b) in enumerate(zip(*outs)):
         assert torch.equal(a, b), k
+
+
+def test_minibatch_gradients_sum_to_full_batch(pkg):
+    """Time-contiguous minibatches (pointer offsets into the tape, same kernels): the two
+    halves' gradients sum to the full batch's under the same per-sample scale."""
+    env, tr = make(pkg, 256, 32, minibatches=2)
+    for name in ("rollout", "critic_values", "advantages"):
+        getattr(tr, name)()
+    M = tr.M
+    got = []
+    for mb in ((0, M // 2), (M // 2, M // 2), (0, M)):
+        tr._mb = mb
+        tr.actor_train()
+        tr.critic_train()
+        torch.cuda.synchronize()
+        got.append(tr.grads.clone())
+    T_ = pkg.trainer
+    ls = slice(T_.OFF["logstd"], T_.OFF["logstd"] + 15)
+    for name in ("W1a", "W2a", "W3a", "W1c", "W2c", "W3c"):
+        a = tr.block(name, got[0]) + tr.block(name, got[1])
+        b = tr.block(name, got[2])
+        assert ((a - b).norm() / b.norm()).item() < 1e-5, name
+    # log_std: the entropy bonus enters every launch once (ent_coef / world)
+    ent = tr.cfg.ent_coef
+    torch.testing.assert_close(got[0][ls] + got[1][ls] + ent, got[2][ls], rtol=1e-5, atol=1e-7)
+
+
+def test_ppo_epochs_engage_the_clip(pkg):
+    """epochs x minibatches > 1: after the first Adam step the ratio leaves 1, so the later
+    minibatches see a nonzero KL and (with a large learning rate) clipped samples."""
+    env, tr = make(pkg, 256, 32, epochs=3, minibatches=4, lr=3e-3)
+    assert "ppo_updates" in tr.phases()
+    p0 = tr.params.clone()
+    tr.iteration()
+    torch.cuda.synchronize()
+    s = tr.loss_stats()
+    assert tr.step_count == 12 and not torch.equal(tr.params, p0)
+    assert abs(s["approx_kl"]) > 1e-7 and s["clip_frac"] > 0.0, s
+    assert all(math.isfinite(v) for v in s.values())

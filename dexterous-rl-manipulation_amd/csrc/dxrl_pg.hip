@@ -808,6 +808,532 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
     }
 }
 
+// ------------------------------------------------------------------ warp-specialised rollout
+// k_pg_rollout_ws: the lane-split rollout with the work that does not depend on this step's
+// env state taken off the env lanes' serial chain.  A workgroup owns 16 envs as in
+// k_pg_rollout_ls, with 8 waves (two per SIMD):
+//   * env waves 0..3: lane (env 4w + row, s) exactly as k_pg_rollout_ls -- observation row,
+//     sampling, dynamics, contacts, termination, auto-reset;
+//   * aux waves 4..7: wave 4 + w is the lane-for-lane twin of env wave w.  While the env lanes
+//     step, the twin computes the NEXT step's Philox draws (action noise, dynamics noise,
+//     observation noise, the reset uniforms for both possible reset counters) and settles the
+//     PREVIOUS step's dense reward and episode bookkeeping (return, records, sums) from the
+//     inputs the env lanes left in LDS;
+//   * all 8 waves split the actor MLP: one 32-column tile of L1 and of L2 each (two waves per
+//     SIMD, so one wave's tanh epilogue overlaps the other's MFMAs); aux wave 7 runs the mu head.
+// Every value is computed by the same instruction sequence as in k_pg_rollout_ls (same MFMA
+// tiles and K order, same Philox calls, same reward ops), so the tapes are bit-identical.
+// Exchanges inside an env's 16 lanes are DPP row broadcasts (an env is one DPP row).
+constexpr int kWsWaves = 8, kWsThreads = 64 * kWsWaves;
+
+// Workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding
+// global store (s_waitcnt vmcnt(0)) before s_barrier, which puts the tape stores' write
+// latency on each step's critical path.  Nothing here is handed between waves through global
+// memory, so only LDS is fenced.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t row_bcast_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x150 + K, 0xF, 0xF, false);  // row_newbcast:K
+}
+template <int K>
+__device__ __forceinline__ float row_bcast(float x) {
+    return __uint_as_float(row_bcast_u32<K>(__float_as_uint(x)));
+}
+template <int K>
+__device__ __forceinline__ double row_bcast(double x) {
+    const uint64_t u = (uint64_t)__double_as_longlong(x);
+    const uint64_t lo = row_bcast_u32<K>((uint32_t)u), hi = row_bcast_u32<K>((uint32_t)(u >> 32));
+    return __longlong_as_double((long long)((hi << 32) | lo));
+}
+// acc = ((acc + x_0) + x_1) + ... + x_{N-1} with x_k = lane k's x (the reference's sequential order)
+template <int N, int K = 0>
+__device__ __forceinline__ void row_sum_in_order(float x, float& acc) {
+    if constexpr (K < N) {
+        acc += row_bcast<K>(x);
+        row_sum_in_order<N, K + 1>(x, acc);
+    }
+}
+template <int K = 0>
+__device__ __forceinline__ void row_joints(float jp, float (&J)[kD]) {
+    if constexpr (K < kD) {
+        J[K] = row_bcast<K>(jp);
+        row_joints<K + 1>(jp, J);
+    }
+}
+// Lane-split contacts_of (ME:285-310) over a DPP row: lane f < 5 computes finger f from the three
+// joint positions of lanes 3f..3f+2; every lane gets the mask (ballot) and the minimum distance.
+__device__ __forceinline__ uint32_t row_contacts(float jp, const double op[3], double size, int s, int gbit,
+                                                 double& dmin, float g3[3]) {
+    float J[kD];
+    row_joints(jp, J);
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+        float g = J[j];
+#pragma unroll
+        for (int f = 1; f < kF; ++f) g = s == f ? J[kJ * f + j] : g;
+        g3[j] = g;
+    }
+    float sum = g3[0];
+#pragma unroll
+    for (int j = 1; j < kJ; ++j) sum = sum + g3[j];
+    const double tip = (double)(sum * kC01);
+    const double dx = tip - op[0], dy = tip - op[1], dz = tip - op[2];
+    const double d = sqrt((dx * dx + dy * dy) + dz * dz);
+    const bool hit = s < kF && d < size * 1.5;
+    const uint32_t mask = (uint32_t)(__ballot(hit) >> gbit) & ((1u << kF) - 1u);
+    dmin = row_bcast<0>(d);
+    const double d1 = row_bcast<1>(d), d2 = row_bcast<2>(d), d3 = row_bcast<3>(d), d4 = row_bcast<4>(d);
+    dmin = d1 < dmin ? d1 : dmin;
+    dmin = d2 < dmin ? d2 : dmin;
+    dmin = d3 < dmin ? d3 : dmin;
+    dmin = d4 < dmin ? d4 : dmin;
+    return mask;
+}
+__device__ __forceinline__ void row_object(double opd, double op[3]) {
+    op[0] = row_bcast<0>(opd);
+    op[1] = row_bcast<1>(opd);
+    op[2] = row_bcast<2>(opd);
+}
+
+// observation element k written by lane s (ME:254-264), slot j of at most 4; -1 = none
+__device__ __forceinline__ int ws_obs_elem(int s, int j) {
+    if (j == 0) return s < kD ? s : -1;
+    if (j == 1) return s < kD ? kD + s : -1;
+    if (j == 2) return s < 7 ? 2 * kD + s : (s < 7 + kF ? 2 * kD + 10 + (s - 7) : -1);
+    return s < 3 ? 2 * kD + 7 + s : -1;
+}
+
+// One env lane's draws for one step, computed by its aux twin (structure of arrays over the
+// 256 env lanes, double-buffered by step parity): action / dynamics noise normals, the
+// observation-noise normals of the lane's obs elements (ws_obs_elem), and the reset uniforms at
+// reset counter c (no reset in the step before) and c + 1 (a reset in the step before).
+struct WsDraws {
+    float eps[2][256], dzn[2][256], on[2][4][256];
+    double u1[2][2][256], u2[2][2][256];
+};
+struct WsReward {      // an env's dense-reward inputs and episode end of one step
+    double dmin;
+    uint32_t c, prev;  // contacts, previous contacts (0x100: none)
+    float nacc[kF];    // per finger: sum of its negative joint positions
+    int32_t len;       // episode length after the step
+    int32_t done, te;
+};
+
+__global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p) {
+    constexpr int kRows = 32;
+    __shared__ __attribute__((aligned(16))) bf16 W1s[kH * kW1s];
+    __shared__ __attribute__((aligned(16))) bf16 W3s[kOut * kW3s];
+    __shared__ __attribute__((aligned(16))) bf16 X[kRows * kXs];
+    __shared__ __attribute__((aligned(16))) bf16 H1[kRows * kHs];
+    __shared__ __attribute__((aligned(16))) bf16 H2[kRows * kHs];
+    __shared__ float MU[kLsEnvs * (kOut + 1)];
+    __shared__ float LS[kActPad], SIG[kActPad], ISIG[kActPad];
+    __shared__ WsDraws DR;
+    __shared__ WsReward RW[2][kLsEnvs];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool aux = wave >= 4;
+    const int et_tid = tid & 255;  // the env lane this thread is (env wave) or twins (aux wave)
+    const int eg = et_tid >> 4, s = et_tid & 15, gbit = 16 * (eg & 3);
+    const int64_t n = p.s.n;
+    const int64_t i = (int64_t)blockIdx.x * kLsEnvs + eg;
+    const bool live = i < n;
+    const int64_t T = p.horizon;
+    if (tid < kAct) {
+        const float ls = p.params[kOffLogStd + tid];
+        LS[tid] = ls;
+        SIG[tid] = __expf(ls);
+        ISIG[tid] = __expf(-ls);
+    }
+    WTile<kH / 16> w2;  // this wave's L2 column tile
+    load_wtile(w2, p.wbf + kBfW2a, kHx, 32 * wave, lane);
+    for (int c = tid; c < kH * (kIn / 8); c += kWsThreads) {
+        const int row = c / (kIn / 8), col = 8 * (c % (kIn / 8));
+        *reinterpret_cast<bf16x8*>(W1s + row * kW1s + col) =
+            *reinterpret_cast<const bf16x8*>(p.wbf + kBfW1a + (int64_t)row * kIn + col);
+    }
+    for (int c = tid; c < kOut * (kH / 8); c += kWsThreads) {
+        const int row = c / (kH / 8), col = 8 * (c % (kH / 8));
+        *reinterpret_cast<bf16x8*>(W3s + row * kW3s + col) =
+            *reinterpret_cast<const bf16x8*>(p.wbf + kBfW3a + (int64_t)row * kHx + col);
+    }
+    for (int c = tid; c < kRows * kXs; c += kWsThreads) {
+        const int row = c / kXs, col = c % kXs;
+        X[c] = (row < kLsEnvs && col == kObsIn) ? (bf16)1.0f : (bf16)0.0f;
+    }
+    for (int c = tid; c < (kRows - kLsEnvs) * kHs; c += kWsThreads) {
+        H1[kLsEnvs * kHs + c] = (bf16)0.0f;
+        H2[kLsEnvs * kHs + c] = (bf16)0.0f;
+    }
+    const int r32 = lane & 31, h2 = lane >> 5;
+    const auto w1frag = [&](int, int k) {
+        return *reinterpret_cast<const bf16x8*>(W1s + (32 * wave + r32) * kW1s + 16 * k + 8 * h2);
+    };
+    const auto w2frag = [&](int, int k) { return w2.b[k]; };
+
+    // ---- env-lane state (env waves) / bookkeeping (aux waves); both know the keys and counters
+    float jp = 0.0f, jv = 0.0f;
+    double opd = 0.0;
+    float ovd = 0.0f;
+    uint32_t flags = 0;
+    int32_t et = 0, cfg = 0;
+    double size = 0.0, mass = 0.0, fric = 0.0, ep_ret = 0.0, sum_ret = 0.0;
+    int32_t cnt = 0, sum_len = 0, succ = 0;
+    uint64_t rctr = 0;
+    uint32_t ek0 = 0, ek1 = 0, pk0 = 0, pk1 = 0;
+    if (live) {
+        if (!aux) {
+            if (s < kD) {
+                jp = p.s.jp[(int64_t)s * n + i];
+                jv = p.s.jv[(int64_t)s * n + i];
+            }
+            if (s < 3) {
+                opd = p.s.op[(int64_t)s * n + i];
+                ovd = p.s.ov[(int64_t)s * n + i];
+            }
+            flags = p.s.flags[i];
+            et = p.s.t[i];
+            size = p.s.size[i];
+            mass = p.s.mass[i];
+            fric = p.s.fric[i];
+        } else {
+            ep_ret = p.ep_ret[i];
+        }
+        cfg = p.s.cfg[i];
+        rctr = p.s.reset_ctr[i];
+        env_key(p.env_seed, p.gid0 + i, ek0, ek1);
+        env_key(p.policy_seed, p.gid0 + i, pk0, pk1);
+    }
+    const int s2 = s < DXRL_RESET_EXTRA ? s : 0;
+    double lo2 = 0.0, hi2 = 0.0, cst2 = 0.0;
+    bool has2 = true, fric64 = false;
+    if (live && !aux) {
+        const dxrl_curriculum& cu = p.s.curricula[cfg];
+        const double* rg = s2 == 0 ? cu.size_range
+                                   : s2 == 1 ? cu.mass_range
+                                             : s2 == 2 ? cu.friction_range
+                                                       : s2 == 3 ? cu.spawn_x_range : s2 == 4 ? cu.spawn_y_range : cu.spawn_z_range;
+        lo2 = rg[0];
+        hi2 = rg[1];
+        cst2 = s2 == 0 ? cu.object_size : s2 == 1 ? cu.object_mass : cu.friction_coefficient;
+        has2 = s2 == 0 ? cu.has_size_range != 0 : s2 == 1 ? cu.has_mass_range != 0 : s2 == 2 ? cu.has_friction_range != 0 : true;
+        fric64 = cu.friction_is_f64_scalar != 0;
+    }
+    const int sa = s < kAct ? s : 0;
+    const bool obs_noise = p.obs_noise > 0.0f, dyn_noise = p.dyn_noise > 0.0f;
+    // aux: the draws of one step (Philox counter base ctr) into buffer b.  Each Philox block is
+    // computed once per env row and its values written straight into the LDS slots of the env
+    // lanes that use them (the ls kernel's lanes recompute shared blocks: 16 lanes, 4 distinct
+    // action-noise blocks, 11 reset blocks):
+    //   lanes 0..10: reset block s at counters rc and rc + 1 (slots 2s, 2s + 1: joint slots
+    //                0..14 -> u1 of lane k, extra slots 15..20 -> u2 of lane k - 15);
+    //   lanes 11..14: action- and dynamics-noise block s - 11 (normals 4(s-11) .. +3);
+    //   lanes 0..11: observation-noise block s (obs elements 4s .. 4s + 3).
+    const int rbase = et_tid & ~15;
+    const auto obs_slot = [&](int k, int& ln, int& j) {  // inverse of ws_obs_elem
+        if (k < kD) { ln = k; j = 0; }
+        else if (k < 2 * kD) { ln = k - kD; j = 1; }
+        else if (k < 2 * kD + 7) { ln = k - 2 * kD; j = 2; }
+        else if (k < 2 * kD + 10) { ln = k - 2 * kD - 7; j = 3; }
+        else { ln = 7 + (k - 2 * kD - 10); j = 2; }
+    };
+    const auto normals4 = [&](uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream, int blk, float nz[4]) {
+        const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)blk}, k0, k1);
+        box_muller(r.x, r.y, nz[0], nz[1]);
+        box_muller(r.z, r.w, nz[2], nz[3]);
+    };
+    const auto make_draws = [&](int b, uint64_t ctr, uint64_t rc) {
+        if (s < (kReset + 1) / 2) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint64_t c = rc + q;
+                const u32x4 r = philox(u32x4{(uint32_t)c, (uint32_t)(c >> 32), kStreamReset, (uint32_t)s}, ek0, ek1);
+                const double ua = u01_53(r.x, r.y), ub = u01_53(r.z, r.w);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int k = 2 * s + h;
+                    const double u = h ? ub : ua;
+                    if (k < kD) DR.u1[b][q][rbase + k] = u;
+                    else if (k < kReset) DR.u2[b][q][rbase + k - kD] = u;
+                }
+            }
+        } else if (s < (kReset + 1) / 2 + 4) {
+            const int blk = s - (kReset + 1) / 2;
+            float nz[4];
+            normals4(pk0, pk1, ctr, kStreamPolicy, blk, nz);
+#pragma unroll
+            for (int h = 0; h < 4; ++h)
+                if (4 * blk + h < kAct) DR.eps[b][rbase + 4 * blk + h] = nz[h];
+            if (dyn_noise) {
+                normals4(pk0, pk1, ctr, kStreamDyn, blk, nz);
+#pragma unroll
+                for (int h = 0; h < 4; ++h)
+                    if (4 * blk + h < kAct) DR.dzn[b][rbase + 4 * blk + h] = nz[h];
+            }
+        }
+        if (obs_noise && s < (kObs + 3) / 4) {
+            float nz[4];
+            normals4(pk0, pk1, ctr, kStreamObs, s, nz);
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const int k = 4 * s + h;
+                if (k < kObs) {
+                    int ln, j;
+                    obs_slot(k, ln, j);
+                    DR.on[b][j][rbase + ln] = nz[h];
+                }
+            }
+        }
+    };
+    // aux: the dense reward (RS:50-187) and episode bookkeeping of a settled step
+    const auto settle = [&](int b, int64_t t_) {
+        const WsReward& w = RW[b][eg];
+        const double dist = exp(-5.0 * w.dmin);
+        const double con = (double)__popc(w.c) / (double)kF;
+        float sum = 0.0f;
+#pragma unroll
+        for (int f = 0; f < kF; ++f) sum = sum + (-w.nacc[f]);
+        const float avg = sum / (float)kF;
+        const float clo = clipf(avg / (float)kF, 0.0f, 1.0f);
+        float st = 0.0f;
+        if (w.prev != 0x100u) {
+            float ch = 0.0f;
+#pragma unroll
+            for (int f = 0; f < kF; ++f) ch = ch + (float)(((w.c ^ w.prev) >> f) & 1u);
+            st = clipf(1.0f - ch / (float)kF, 0.0f, 1.0f);
+        }
+        const double r = ((p.w.w_dist * dist + p.w.w_con * con) + p.w.w_clo * (double)clo) + p.w.w_st * (double)st;
+        ep_ret += r;
+        if (s == 0) p.rew[t_ * n + i] = (float)r;
+        if (w.done) {
+            if (s == 0 && cnt < p.record_cap) {
+                const int64_t o = i * p.record_cap + cnt;
+                p.rec_return[o] = ep_ret;
+                p.rec_length[o] = w.len;
+                p.rec_success[o] = p.success_terminated ? (uint8_t)w.te : (uint8_t)0;
+                p.rec_end_step[o] = (int32_t)t_;
+            }
+            ++cnt;
+            sum_ret += ep_ret;
+            sum_len += w.len;
+            succ += w.te;
+            ep_ret = 0.0;
+            ++rctr;
+        }
+    };
+    const auto write_obs_row = [&](int b) {
+        bf16* xr = X + eg * kXs;
+        const auto put = [&](int j, float v) {
+            if (obs_noise) v = v + p.obs_noise * DR.on[b][j][et_tid];
+            xr[ws_obs_elem(s, j)] = to_bf16(v);
+        };
+        if (s < kD) {
+            put(0, jp);
+            put(1, jv);
+        }
+        if (s < 3) {
+            put(2, (float)opd);
+            put(3, ovd);
+        } else if (s < 7) {
+            put(2, s == 3 ? 1.0f : 0.0f);  // identity quaternion (ME:164)
+        } else if (s < 7 + kF) {
+            put(2, (float)((flags >> (s - 7)) & 1u));
+        }
+    };
+    const auto tape_obs_row = [&](int64_t m) {
+        *reinterpret_cast<bf16x4*>(p.obs_rm + m * kIn + 4 * s) = *reinterpret_cast<const bf16x4*>(X + eg * kXs + 4 * s);
+    };
+    const bool mlp = !(p.diag & 1), env_on = !(p.diag & 2);
+    bool prev_reset = false;  // env lanes: did the previous step end an episode (and reset)?
+    const auto env_lane_step = [&](int64_t t, int64_t m, int b) {
+        // ---- env lanes: a = mu + sigma * eps, log pi(a|s) in action order (gauss_logp's order)
+        const float mu = mlp ? MU[eg * (kOut + 1) + sa] : 0.0f;
+        float a = mu + SIG[sa] * DR.eps[b][et_tid];
+        const float z = (a - mu) * ISIG[sa];
+        const float term = -0.5f * z * z - LS[sa] - 0.5f * kLog2Pi;
+        float lp = 0.0f;
+        row_sum_in_order<kAct>(term, lp);
+        p.act[m * kActPad + s] = s < kAct ? a : 0.0f;
+        if (s == 0) p.logp[m] = lp;
+        if (dyn_noise)  // robustness_tests.py:180-187 (the tape keeps the policy's action)
+            a = clipf(a + p.dyn_noise * DR.dzn[b][et_tid], -1.0f, 1.0f);
+        if (p.applied_act) p.applied_act[m * kActPad + s] = s < kAct ? a : 0.0f;
+        bool te = false, tr = false;
+        if (env_on) {
+            // ---- env_step, lane-split (ME:198-252)
+            if (s < kD) {
+                const float ak = clipf(a, -1.0f, 1.0f);
+                jv = kC09 * jv + kC01 * ak;
+                jp = clipf(jp + jv * kDt, -1.0f, 1.0f);
+            }
+            {
+                const double damp = 1.0 - (fric * 0.1 * 0.01);
+                const float dampf = (float)damp;
+                const bool op32 = (flags & kOpIsF32) != 0, fric_f64 = (flags & kFricF64) != 0;
+                const int ax = s < 3 ? s : 0;
+                const double gz = ax == 2 ? kGz : 0.0, lo = ax == 2 ? 0.0 : -0.2, hi = ax == 2 ? 0.3 : 0.2;
+                float v = fric_f64 ? (float)((double)ovd * damp) : ovd * dampf;
+                v = (float)((double)v + gz);
+                const float inc = v * kDt;
+                double q = op32 ? (double)((float)opd + inc) : opd + (double)inc;
+                q = clipd(q, lo, hi);
+                if ((q <= lo && v < 0.0f) || (q >= hi && v > 0.0f)) v = 0.0f;
+                if (s < 3) {
+                    opd = q;
+                    ovd = v;
+                }
+            }
+            flags &= ~kOpIsF32;
+            double op3[3];
+            row_object(opd, op3);
+            double dmin;
+            float g3[3];
+            const uint32_t c = row_contacts(jp, op3, size, s, gbit, dmin, g3);
+            // the reward's inputs for the aux twin (RS:101-187)
+            WsReward& rw = RW[b][eg];
+            float nacc = 0.0f;
+#pragma unroll
+            for (int j = 0; j < kJ; ++j)
+                if (g3[j] < 0.0f) nacc = nacc + g3[j];
+            if (s < kF) rw.nacc[s] = nacc;
+            if (s == 0) {
+                rw.dmin = dmin;
+                rw.c = c;
+                rw.prev = (flags & kHasPrev) ? ((flags >> kPrevShift) & 0xFFu) : 0x100u;
+            }
+            flags = (flags & ~(0xFFu << kPrevShift)) | (c << kPrevShift) | kHasPrev;
+            flags = (flags & ~0xFFu) | c;
+            te = __popc(c) >= 3;
+            tr = et >= p.max_episode_steps;
+            et += 1;
+        }
+        const bool d = env_on && (te || tr || et >= p.max_steps);
+        if (s == 0) {
+            p.done[m] = d;
+            if (p.ep_code)
+                p.ep_code[m] = d ? (uint16_t)((et << 1) | (p.success_terminated && te ? 1 : 0)) : (uint16_t)0;
+            WsReward& rw = RW[b][eg];
+            rw.done = d;
+            rw.te = te;
+            rw.len = et;
+        }
+        if (d) {
+            // ---- env_reset_philox, lane-split: lane s holds slot s (joint) and slot 15 + s
+            const int q = prev_reset ? 1 : 0;  // the reset counter this step sees (DR.u1 [q])
+            const double u1 = DR.u1[b][q][et_tid], u2 = DR.u2[b][q][et_tid];
+            const double v2 = has2 ? lo2 + (hi2 - lo2) * u2 : cst2;  // config.py:44-113 samplers
+            if (s < kD) {
+                jp = (float)(-0.1 + (0.1 - -0.1) * u1);
+                jv = 0.0f;
+            }
+            size = row_bcast<0>(v2);
+            mass = row_bcast<1>(v2);
+            fric = row_bcast<2>(v2);
+            const double sx = row_bcast<3>(v2), sy = row_bcast<4>(v2), sz = row_bcast<5>(v2);
+            const double spawn = s == 1 ? sy : (s == 2 ? sz : sx);
+            const bool has = (flags & kHasObject) != 0;
+            if (s < 3) {
+                opd = (double)(float)(has ? opd : spawn);
+                ovd = 0.0f;
+            }
+            et = 0;
+            flags = kOpIsF32 | kHasObject | (fric64 ? kFricF64 : 0u);
+            double op3[3];
+            row_object(opd, op3);
+            double dmin;
+            float g3[3];
+            flags |= row_contacts(jp, op3, size, s, gbit, dmin, g3);
+            ++rctr;
+        }
+        prev_reset = d;
+    };
+    if (aux && live) make_draws(0, p.iteration * (uint64_t)T, rctr);
+    __syncthreads();
+    for (int64_t t = 0; t < T; ++t) {
+        const int64_t m = t * n + i;
+        const int b = (int)(t & 1);
+        if (!aux && live) write_obs_row(b);
+        lds_barrier();
+        if (!aux && live) tape_obs_row(m);
+        if (mlp) wave_layer<kIn / 16, 1, true, 1>(X, kXs, w1frag, 32 * wave, nullptr, 0, H1, kHs, lane);
+        lds_barrier();
+        if (mlp)
+            wave_layer<kH / 16, 1, true, 1>(H1, kHs, w2frag, 32 * wave, p.params + kOffW2a + kH, kHx, H2, kHs, lane);
+        lds_barrier();
+        if (mlp && wave == kWsWaves - 1) {  // mu head: 16 env rows x 32 head rows
+            f32x16 acc;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+            // H2 rows and W3 rows (head outputs) from LDS, 4 k-steps of fragments in flight
+#pragma unroll
+            for (int k0 = 0; k0 < kH / 16; k0 += 4) {
+                bf16x8 ah[4], bw[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    ah[k] = *reinterpret_cast<const bf16x8*>(H2 + r32 * kHs + 16 * (k0 + k) + 8 * h2);
+                    bw[k] = *reinterpret_cast<const bf16x8*>(W3s + r32 * kW3s + 16 * (k0 + k) + 8 * h2);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc = mfma32(ah[k], bw[k], acc);
+            }
+            const float bias = p.params[kOffW3a + (int64_t)r32 * kHx + kH];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) MU[acc_row(q, lane) * (kOut + 1) + r32] = acc[q] + bias;  // rows < 16
+        }
+        lds_barrier();
+        if (live && aux) {
+            // the previous step's reward and bookkeeping (its inputs were left before the last
+            // barriers), then the next step's draws at the counter that step will see
+            if (t > 0 && env_on) settle(b ^ 1, t - 1);
+            make_draws(b ^ 1, p.iteration * (uint64_t)T + (uint64_t)(t + 1), rctr);
+        } else if (live) {
+            env_lane_step(t, m, b);
+        }
+        lds_barrier();  // next step's draws / this step's reward inputs visible
+    }
+    __syncthreads();
+    const int bT = (int)(T & 1);
+    if (live && aux) {
+        if (T > 0 && env_on) settle(bT ^ 1, T - 1);
+        if (p.diag & 2)
+            for (int64_t t = 0; t < T && s == 0; ++t) p.rew[t * n + i] = 0.0f;
+        if (s == 0) {
+            p.ep_ret[i] = ep_ret;
+            p.ep_count[i] = cnt;
+            p.ep_sum_ret[i] = sum_ret;
+            p.ep_sum_len[i] = sum_len;
+            p.ep_succ[i] = succ;
+        }
+    }
+    if (live && !aux) {
+        // bootstrap observation (slot T), then the state back to the slab
+        write_obs_row(bT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        tape_obs_row(T * n + i);
+        if (s < kD) {
+            p.s.jp[(int64_t)s * n + i] = jp;
+            p.s.jv[(int64_t)s * n + i] = jv;
+        }
+        if (s < 3) {
+            p.s.op[(int64_t)s * n + i] = opd;
+            p.s.ov[(int64_t)s * n + i] = ovd;
+        }
+        if (s == 0) {
+            p.s.flags[i] = flags;
+            p.s.t[i] = et;
+            p.s.size[i] = size;
+            p.s.mass[i] = mass;
+            p.s.fric[i] = fric;
+            p.s.reset_ctr[i] = rctr;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ GAE
 // delta_t = r_t + gamma V_{t+1} (1 - d_t) - V_t ; A_t = delta_t + gamma lambda (1 - d_t) A_{t+1}
 // One thread per env scans t = T-1 .. 0 (coalesced across envs), 64-env workgroups so the scan
@@ -1213,6 +1739,11 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
         hipLaunchKernelGGL(k_pg_rollout, dim3((unsigned)((n + kTile - 1) / kTile)), dim3(64 * kRolloutWaves), 0,
                            as_stream(stream), p);
         return launch_check("k_pg_rollout");
+    }
+    if (!(a->diag_flags & (32 | 64))) {  // default: the warp-specialised kernel
+        hipLaunchKernelGGL(k_pg_rollout_ws, dim3((unsigned)((n + kLsEnvs - 1) / kLsEnvs)), dim3(kWsThreads), 0,
+                           as_stream(stream), p);
+        return launch_check("k_pg_rollout_ws");
     }
     static unsigned long long* stamps = nullptr;
     static int64_t stamps_n = 0;

@@ -299,12 +299,13 @@ def test_fused_dynamics_noise(pkg, std):
 @pytest.mark.parametrize("cur,n,noise", [("easy", 96, 0.0), ("variable", 100, 0.0), ("hard", 64, 0.05),
                                          ("variable", 4100, 0.05)])
 def test_lane_split_rollout_matches_64_env_kernel(pkg, cur, n, noise):
-    """k_pg_rollout_ls (16 envs x 16 lanes per workgroup) and k_pg_rollout (one lane per env)
-    share every Philox stream and every op: tapes, episode records and env state are equal bit
-    for bit (including auto-resets, observation / dynamics noise and a ragged last workgroup)."""
+    """k_pg_rollout_ws (default: 16 envs x 16 lanes, env waves + aux twin waves, 8 waves),
+    k_pg_rollout_ls (diag 64: the same lanes on 4 waves) and k_pg_rollout (diag 16: one lane
+    per env) share every Philox stream and every op: tapes, episode records and env state are
+    equal bit for bit (auto-resets, observation / dynamics noise, a ragged last workgroup)."""
     T = 24
     outs = []
-    for diag in (16, 0):
+    for diag in (16, 64, 0):
         env = pkg.envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.named(cur), reward_type="dense", seed=11)
         cfg = pkg.trainer.TrainerConfig(horizon=T, seed=5, max_steps=13, record_cap=T, obs_noise_std=noise,
                                         dyn_noise_std=noise)
@@ -319,8 +320,9 @@ def test_lane_split_rollout_matches_64_env_kernel(pkg, cur, n, noise):
                                           tr.rec_return, tr.rec_length, tr.rec_end, env.joint_positions,
                                           env.joint_velocities, env.object_position, env.object_velocity, env.flags,
                                           env.step_count, env.object_size, env.friction_coefficient)])
-    for k, (a, b) in enumerate(zip(*outs)):
-        assert torch.equal(a, b), k
+    for other in outs[1:]:
+        for k, (a, b) in enumerate(zip(outs[0], other)):
+            assert torch.equal(a, b), k
 
 
 def test_minibatch_gradients_sum_to_full_batch(pkg):

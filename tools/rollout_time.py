@@ -1,4 +1,4 @@
-"""Time the fused PG rollout with parts switched off (diag flags) at the bench shape."""
+"""Time the fused PG rollout kernels (ws default, ls = diag 64) at the bench shape, one line."""
 import os
 import sys
 
@@ -9,19 +9,21 @@ import dexterous_rl_manipulation_amd as pkg  # noqa: E402
 from dexterous_rl_manipulation_amd import envs, trainer  # noqa: E402
 
 dev = torch.device("cuda:0")
-for cur in ("easy", "hard"):
+cur = os.environ.get("CUR", "easy")
+out = []
+for noise in (0.0, 0.05):
     env = envs.VecEnv(4096, curriculum_config=pkg.CurriculumConfig.named(cur), reward_type="dense", seed=1, device=dev)
-    tr = trainer.PGTrainer(env, trainer.TrainerConfig(horizon=200, seed=7))
+    tr = trainer.PGTrainer(env, trainer.TrainerConfig(horizon=200, seed=7, obs_noise_std=noise, dyn_noise_std=noise))
     env.reset(write_obs=False)
-    for flags, name in ((0, "ws full"), (1, "ws no-MLP"), (2, "ws no-env"), (3, "ws neither"), (64, "ls full"),
-                        (65, "ls no-MLP"), (66, "ls no-env"), (67, "ls neither")):
+    for flags, name in ((0, "ws"), (64, "ls")):
         tr.diag_flags = flags
         tr.rollout()
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        for _ in range(5):
+        for _ in range(10):
             tr.rollout()
         b.record()
         torch.cuda.synchronize()
-        print(f"{cur:5s} {name:8s} {a.elapsed_time(b) / 5:8.3f} ms")
+        out.append(f"{name}{'+noise' if noise else ''}={a.elapsed_time(b) / 10:.3f}")
+print(cur, " ".join(out))

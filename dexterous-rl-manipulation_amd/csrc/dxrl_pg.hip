@@ -908,13 +908,15 @@ __device__ __forceinline__ int ws_obs_elem(int s, int j) {
     return s < 3 ? 2 * kD + 7 + s : -1;
 }
 
-// One env lane's draws for one step, computed by its aux twin (structure of arrays over the
-// 256 env lanes, double-buffered by step parity): action / dynamics noise normals, the
-// observation-noise normals of the lane's obs elements (ws_obs_elem), and the reset uniforms at
-// reset counter c (no reset in the step before) and c + 1 (a reset in the step before).
+// One env lane's draws, computed by its aux twin (structure of arrays over the 256 env lanes):
+// the action / dynamics noise normals and the reset uniforms (at the env's exact reset counter)
+// of the current step, and the observation-noise normals of the lane's obs elements
+// (ws_obs_elem) for the next observation row.  Single-buffered: each is written in the head
+// phase and read before the next head phase.  The reward inputs (WsReward) are double-buffered
+// by step parity: the env lanes write step t's while the aux lanes settle step t-1's.
 struct WsDraws {
-    float eps[2][256], dzn[2][256], on[2][4][256];
-    double u1[2][2][256], u2[2][2][256];
+    float eps[256], dzn[256], on[4][256];
+    double u1[256], u2[256];
 };
 struct WsReward {      // an env's dense-reward inputs and episode end of one step
     double dmin;
@@ -924,8 +926,18 @@ struct WsReward {      // an env's dense-reward inputs and episode end of one st
     int32_t done, te;
 };
 
+// Step t of a workgroup (16 envs, 8 waves):
+//   P0  env lanes write the observation row (+ observation noise drawn in step t-1's P3)
+//   P1  all waves: L1, one 32-column tile each            (the env lanes also store the obs row)
+//   P2  all waves: L2, one 32-column tile each
+//   P3  env wave 3: the mu head.  Aux lanes, in that shadow: settle step t-1's reward and
+//       bookkeeping, then draw step t's action / dynamics noise and reset uniforms (the reset
+//       counter is exact now: step t-1's episode end is known) and step t+1's observation noise
+//   P4  env lanes: a = mu + sigma eps, dynamics, contacts, termination, auto-reset.
+//       Aux lanes: the same a, log pi (DPP row sum in action order), the act / log pi tape
 __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p) {
     constexpr int kRows = 32;
+    constexpr int kHeadWave = 3;  // an env wave: the env lanes idle while the head runs
     __shared__ __attribute__((aligned(16))) bf16 W1s[kH * kW1s];
     __shared__ __attribute__((aligned(16))) bf16 W3s[kOut * kW3s];
     __shared__ __attribute__((aligned(16))) bf16 X[kRows * kXs];
@@ -939,6 +951,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     const bool aux = wave >= 4;
     const int et_tid = tid & 255;  // the env lane this thread is (env wave) or twins (aux wave)
     const int eg = et_tid >> 4, s = et_tid & 15, gbit = 16 * (eg & 3);
+    const int rbase = et_tid & ~15;
     const int64_t n = p.s.n;
     const int64_t i = (int64_t)blockIdx.x * kLsEnvs + eg;
     const bool live = i < n;
@@ -975,7 +988,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     };
     const auto w2frag = [&](int, int k) { return w2.b[k]; };
 
-    // ---- env-lane state (env waves) / bookkeeping (aux waves); both know the keys and counters
+    // ---- env-lane state (env waves) / episode bookkeeping (aux waves)
     float jp = 0.0f, jv = 0.0f;
     double opd = 0.0;
     float ovd = 0.0f;
@@ -1025,73 +1038,88 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     }
     const int sa = s < kAct ? s : 0;
     const bool obs_noise = p.obs_noise > 0.0f, dyn_noise = p.dyn_noise > 0.0f;
-    // aux: the draws of one step (Philox counter base ctr) into buffer b.  Each Philox block is
-    // computed once per env row and its values written straight into the LDS slots of the env
-    // lanes that use them (the ls kernel's lanes recompute shared blocks: 16 lanes, 4 distinct
-    // action-noise blocks, 11 reset blocks):
-    //   lanes 0..10: reset block s at counters rc and rc + 1 (slots 2s, 2s + 1: joint slots
-    //                0..14 -> u1 of lane k, extra slots 15..20 -> u2 of lane k - 15);
-    //   lanes 11..14: action- and dynamics-noise block s - 11 (normals 4(s-11) .. +3);
-    //   lanes 0..11: observation-noise block s (obs elements 4s .. 4s + 3).
-    const int rbase = et_tid & ~15;
+
+    // ---- aux: Philox draws.  Each block is computed once per env row and its values written
+    // straight into the LDS slots of the env lanes that use them (k_pg_rollout_ls recomputes the
+    // shared blocks on every lane): lanes 0..10 reset block s (slots 2s, 2s + 1: joint slots 0..14
+    // -> u1 of lane k, extra slots 15..20 -> u2 of lane k - 15); lanes 11..14 action- and
+    // dynamics-noise block s - 11 (normals 4(s-11) .. +3); lanes 0..11 observation-noise block s
+    // (obs elements 4s .. 4s + 3).  Same blocks and arithmetic as philox_normal_at /
+    // reset_uniform_at, so the values are identical.
     const auto obs_slot = [&](int k, int& ln, int& j) {  // inverse of ws_obs_elem
-        if (k < kD) { ln = k; j = 0; }
-        else if (k < 2 * kD) { ln = k - kD; j = 1; }
-        else if (k < 2 * kD + 7) { ln = k - 2 * kD; j = 2; }
-        else if (k < 2 * kD + 10) { ln = k - 2 * kD - 7; j = 3; }
-        else { ln = 7 + (k - 2 * kD - 10); j = 2; }
+        if (k < kD) {
+            ln = k;
+            j = 0;
+        } else if (k < 2 * kD) {
+            ln = k - kD;
+            j = 1;
+        } else if (k < 2 * kD + 7) {
+            ln = k - 2 * kD;
+            j = 2;
+        } else if (k < 2 * kD + 10) {
+            ln = k - 2 * kD - 7;
+            j = 3;
+        } else {
+            ln = 7 + (k - 2 * kD - 10);
+            j = 2;
+        }
     };
-    const auto normals4 = [&](uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream, int blk, float nz[4]) {
-        const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)blk}, k0, k1);
+    const auto normals4 = [&](uint64_t ctr, uint32_t stream, int blk, float nz[4]) {
+        const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)blk}, pk0, pk1);
         box_muller(r.x, r.y, nz[0], nz[1]);
         box_muller(r.z, r.w, nz[2], nz[3]);
     };
-    const auto make_draws = [&](int b, uint64_t ctr, uint64_t rc) {
-        if (s < (kReset + 1) / 2) {
+    constexpr int kResetBlocks = (kReset + 1) / 2;
+    const auto step_draws = [&](uint64_t ctr, uint64_t rc) {  // step ctr's noise, reset at counter rc
+        // one Philox call for the whole wave (lanes 0..10 a reset block, 11..14 an action-noise
+        // block), then per-lane conversion and scatter
+        const bool rs = s < kResetBlocks;
+        const int blk = rs ? s : s - kResetBlocks;
+        const uint64_t c = rs ? rc : ctr;
+        const u32x4 r = philox(u32x4{(uint32_t)c, (uint32_t)(c >> 32), rs ? kStreamReset : kStreamPolicy, (uint32_t)blk},
+                               rs ? ek0 : pk0, rs ? ek1 : pk1);
+        if (rs) {
+            const double ua = u01_53(r.x, r.y), ub = u01_53(r.z, r.w);
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint64_t c = rc + q;
-                const u32x4 r = philox(u32x4{(uint32_t)c, (uint32_t)(c >> 32), kStreamReset, (uint32_t)s}, ek0, ek1);
-                const double ua = u01_53(r.x, r.y), ub = u01_53(r.z, r.w);
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int k = 2 * s + h;
-                    const double u = h ? ub : ua;
-                    if (k < kD) DR.u1[b][q][rbase + k] = u;
-                    else if (k < kReset) DR.u2[b][q][rbase + k - kD] = u;
-                }
+            for (int h = 0; h < 2; ++h) {
+                const int k = 2 * s + h;
+                const double u = h ? ub : ua;
+                if (k < kD) DR.u1[rbase + k] = u;
+                else if (k < kReset) DR.u2[rbase + k - kD] = u;
             }
-        } else if (s < (kReset + 1) / 2 + 4) {
-            const int blk = s - (kReset + 1) / 2;
+        } else if (blk < 4) {
             float nz[4];
-            normals4(pk0, pk1, ctr, kStreamPolicy, blk, nz);
+            box_muller(r.x, r.y, nz[0], nz[1]);
+            box_muller(r.z, r.w, nz[2], nz[3]);
 #pragma unroll
             for (int h = 0; h < 4; ++h)
-                if (4 * blk + h < kAct) DR.eps[b][rbase + 4 * blk + h] = nz[h];
+                if (4 * blk + h < kAct) DR.eps[rbase + 4 * blk + h] = nz[h];
             if (dyn_noise) {
-                normals4(pk0, pk1, ctr, kStreamDyn, blk, nz);
+                normals4(ctr, kStreamDyn, blk, nz);
 #pragma unroll
                 for (int h = 0; h < 4; ++h)
-                    if (4 * blk + h < kAct) DR.dzn[b][rbase + 4 * blk + h] = nz[h];
+                    if (4 * blk + h < kAct) DR.dzn[rbase + 4 * blk + h] = nz[h];
             }
         }
+    };
+    const auto obs_draws = [&](uint64_t ctr) {  // the observation noise of row ctr
         if (obs_noise && s < (kObs + 3) / 4) {
             float nz[4];
-            normals4(pk0, pk1, ctr, kStreamObs, s, nz);
+            normals4(ctr, kStreamObs, s, nz);
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
                 const int k = 4 * s + h;
                 if (k < kObs) {
                     int ln, j;
                     obs_slot(k, ln, j);
-                    DR.on[b][j][rbase + ln] = nz[h];
+                    DR.on[j][rbase + ln] = nz[h];
                 }
             }
         }
     };
-    // aux: the dense reward (RS:50-187) and episode bookkeeping of a settled step
-    const auto settle = [&](int b, int64_t t_) {
-        const WsReward& w = RW[b][eg];
+    // ---- aux: the dense reward (RS:50-187) and the episode bookkeeping of a finished step
+    const auto settle = [&](int64_t t_) {
+        const WsReward& w = RW[t_ & 1][eg];
         const double dist = exp(-5.0 * w.dmin);
         const double con = (double)__popc(w.c) / (double)kF;
         float sum = 0.0f;
@@ -1122,13 +1150,12 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             sum_len += w.len;
             succ += w.te;
             ep_ret = 0.0;
-            ++rctr;
         }
     };
-    const auto write_obs_row = [&](int b) {
+    const auto write_obs_row = [&]() {
         bf16* xr = X + eg * kXs;
         const auto put = [&](int j, float v) {
-            if (obs_noise) v = v + p.obs_noise * DR.on[b][j][et_tid];
+            if (obs_noise) v = v + p.obs_noise * DR.on[j][et_tid];
             xr[ws_obs_elem(s, j)] = to_bf16(v);
         };
         if (s < kD) {
@@ -1148,20 +1175,12 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         *reinterpret_cast<bf16x4*>(p.obs_rm + m * kIn + 4 * s) = *reinterpret_cast<const bf16x4*>(X + eg * kXs + 4 * s);
     };
     const bool mlp = !(p.diag & 1), env_on = !(p.diag & 2);
-    bool prev_reset = false;  // env lanes: did the previous step end an episode (and reset)?
-    const auto env_lane_step = [&](int64_t t, int64_t m, int b) {
-        // ---- env lanes: a = mu + sigma * eps, log pi(a|s) in action order (gauss_logp's order)
+    // ---- env lanes, P4 of step t: action, dynamics, contacts, termination, auto-reset
+    const auto env_lane_step = [&](int64_t t, int64_t m) {
         const float mu = mlp ? MU[eg * (kOut + 1) + sa] : 0.0f;
-        float a = mu + SIG[sa] * DR.eps[b][et_tid];
-        const float z = (a - mu) * ISIG[sa];
-        const float term = -0.5f * z * z - LS[sa] - 0.5f * kLog2Pi;
-        float lp = 0.0f;
-        row_sum_in_order<kAct>(term, lp);
-        p.act[m * kActPad + s] = s < kAct ? a : 0.0f;
-        if (s == 0) p.logp[m] = lp;
+        float a = mu + SIG[sa] * DR.eps[et_tid];
         if (dyn_noise)  // robustness_tests.py:180-187 (the tape keeps the policy's action)
-            a = clipf(a + p.dyn_noise * DR.dzn[b][et_tid], -1.0f, 1.0f);
-        if (p.applied_act) p.applied_act[m * kActPad + s] = s < kAct ? a : 0.0f;
+            a = clipf(a + p.dyn_noise * DR.dzn[et_tid], -1.0f, 1.0f);
         bool te = false, tr = false;
         if (env_on) {
             // ---- env_step, lane-split (ME:198-252)
@@ -1194,7 +1213,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             float g3[3];
             const uint32_t c = row_contacts(jp, op3, size, s, gbit, dmin, g3);
             // the reward's inputs for the aux twin (RS:101-187)
-            WsReward& rw = RW[b][eg];
+            WsReward& rw = RW[t & 1][eg];
             float nacc = 0.0f;
 #pragma unroll
             for (int j = 0; j < kJ; ++j)
@@ -1216,15 +1235,14 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             p.done[m] = d;
             if (p.ep_code)
                 p.ep_code[m] = d ? (uint16_t)((et << 1) | (p.success_terminated && te ? 1 : 0)) : (uint16_t)0;
-            WsReward& rw = RW[b][eg];
+            WsReward& rw = RW[t & 1][eg];
             rw.done = d;
             rw.te = te;
             rw.len = et;
         }
         if (d) {
             // ---- env_reset_philox, lane-split: lane s holds slot s (joint) and slot 15 + s
-            const int q = prev_reset ? 1 : 0;  // the reset counter this step sees (DR.u1 [q])
-            const double u1 = DR.u1[b][q][et_tid], u2 = DR.u2[b][q][et_tid];
+            const double u1 = DR.u1[et_tid], u2 = DR.u2[et_tid];
             const double v2 = has2 ? lo2 + (hi2 - lo2) * u2 : cst2;  // config.py:44-113 samplers
             if (s < kD) {
                 jp = (float)(-0.1 + (0.1 - -0.1) * u1);
@@ -1249,22 +1267,57 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             flags |= row_contacts(jp, op3, size, s, gbit, dmin, g3);
             ++rctr;
         }
-        prev_reset = d;
     };
-    if (aux && live) make_draws(0, p.iteration * (uint64_t)T, rctr);
+    // ---- aux lanes, P4 of step t: the policy sample, log pi(a|s) (gauss_logp's order), tapes
+    const auto aux_lane_step = [&](int64_t m) {
+        const float mu = mlp ? MU[eg * (kOut + 1) + sa] : 0.0f;
+        float a = mu + SIG[sa] * DR.eps[et_tid];
+        const float z = (a - mu) * ISIG[sa];
+        const float term = -0.5f * z * z - LS[sa] - 0.5f * kLog2Pi;
+        float lp = 0.0f;
+        row_sum_in_order<kAct>(term, lp);
+        p.act[m * kActPad + s] = s < kAct ? a : 0.0f;
+        if (s == 0) p.logp[m] = lp;
+        if (p.applied_act) {
+            if (dyn_noise) a = clipf(a + p.dyn_noise * DR.dzn[et_tid], -1.0f, 1.0f);
+            p.applied_act[m * kActPad + s] = s < kAct ? a : 0.0f;
+        }
+    };
+
+    // diag & 128: s_memtime segment stamps per step (diagnostics only): env waves into
+    // stamps[16 i + k], aux waves into stamps[16 i + 8 + k]
+    unsigned long long st_acc[8], st_last = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) st_acc[q] = 0;
+#define WS_STAMP(k)                                                                              \
+    do {                                                                                         \
+        if (p.diag & 128) {                                                                      \
+            __builtin_amdgcn_sched_barrier(0);                                                   \
+            unsigned long long t_;                                                               \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+            __builtin_amdgcn_sched_barrier(0);                                                   \
+            st_acc[k] += t_ - st_last;                                                           \
+            st_last = t_;                                                                        \
+        }                                                                                        \
+    } while (0)
+    if (aux && live) obs_draws(p.iteration * (uint64_t)T);
     __syncthreads();
+    WS_STAMP(7);
     for (int64_t t = 0; t < T; ++t) {
         const int64_t m = t * n + i;
-        const int b = (int)(t & 1);
-        if (!aux && live) write_obs_row(b);
+        const uint64_t ctr = p.iteration * (uint64_t)T + (uint64_t)t;
+        if (!aux && live) write_obs_row();
+        WS_STAMP(0);
         lds_barrier();
         if (!aux && live) tape_obs_row(m);
         if (mlp) wave_layer<kIn / 16, 1, true, 1>(X, kXs, w1frag, 32 * wave, nullptr, 0, H1, kHs, lane);
+        WS_STAMP(1);
         lds_barrier();
         if (mlp)
             wave_layer<kH / 16, 1, true, 1>(H1, kHs, w2frag, 32 * wave, p.params + kOffW2a + kH, kHx, H2, kHs, lane);
+        WS_STAMP(2);
         lds_barrier();
-        if (mlp && wave == kWsWaves - 1) {  // mu head: 16 env rows x 32 head rows
+        if (mlp && wave == kHeadWave) {  // mu head: 16 env rows x 32 head rows
             f32x16 acc;
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
@@ -1284,21 +1337,35 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
 #pragma unroll
             for (int q = 0; q < 8; ++q) MU[acc_row(q, lane) * (kOut + 1) + r32] = acc[q] + bias;  // rows < 16
         }
-        lds_barrier();
-        if (live && aux) {
-            // the previous step's reward and bookkeeping (its inputs were left before the last
-            // barriers), then the next step's draws at the counter that step will see
-            if (t > 0 && env_on) settle(b ^ 1, t - 1);
-            make_draws(b ^ 1, p.iteration * (uint64_t)T + (uint64_t)(t + 1), rctr);
-        } else if (live) {
-            env_lane_step(t, m, b);
+        if (aux && live) {
+            // this step's draws at the reset counter it sees (step t-1's episode end is known:
+            // its inputs were left before the last barriers), the next observation row's noise
+            if (t > 0 && env_on && RW[(t - 1) & 1][eg].done) ++rctr;
+            step_draws(ctr, rctr);
+            obs_draws(ctr + 1);
         }
-        lds_barrier();  // next step's draws / this step's reward inputs visible
+        WS_STAMP(3);
+        lds_barrier();
+        WS_STAMP(4);
+        if (live) {
+            if (aux) {
+                aux_lane_step(m);
+                if (t > 0 && env_on) settle(t - 1);  // step t-1's reward and bookkeeping
+            } else {
+                env_lane_step(t, m);
+            }
+        }
+        WS_STAMP(5);
+        lds_barrier();  // this step's reward inputs / the next row's noise visible
+        WS_STAMP(6);
     }
-    __syncthreads();
-    const int bT = (int)(T & 1);
+#undef WS_STAMP
+    if ((p.diag & 128) && s == 0 && live) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) p.stamps[16 * i + (aux ? 8 : 0) + q] = st_acc[q];
+    }
     if (live && aux) {
-        if (T > 0 && env_on) settle(bT ^ 1, T - 1);
+        if (T > 0 && env_on) settle(T - 1);
         if (p.diag & 2)
             for (int64_t t = 0; t < T && s == 0; ++t) p.rew[t * n + i] = 0.0f;
         if (s == 0) {
@@ -1311,7 +1378,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     }
     if (live && !aux) {
         // bootstrap observation (slot T), then the state back to the slab
-        write_obs_row(bT);
+        write_obs_row();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         tape_obs_row(T * n + i);
@@ -1740,19 +1807,34 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                            as_stream(stream), p);
         return launch_check("k_pg_rollout");
     }
-    if (!(a->diag_flags & (32 | 64))) {  // default: the warp-specialised kernel
-        hipLaunchKernelGGL(k_pg_rollout_ws, dim3((unsigned)((n + kLsEnvs - 1) / kLsEnvs)), dim3(kWsThreads), 0,
-                           as_stream(stream), p);
-        return launch_check("k_pg_rollout_ws");
-    }
     static unsigned long long* stamps = nullptr;
     static int64_t stamps_n = 0;
-    if ((a->diag_flags & 32) && stamps_n < n) {
+    if ((a->diag_flags & (32 | 128)) && stamps_n < n) {
         if (stamps) (void)hipFree(stamps);
-        (void)hipMalloc(&stamps, (size_t)n * 8 * sizeof(unsigned long long));
+        (void)hipMalloc(&stamps, (size_t)n * 16 * sizeof(unsigned long long));
         stamps_n = n;
     }
     p.stamps = stamps;
+    if (!(a->diag_flags & (32 | 64))) {  // default: the warp-specialised kernel
+        hipLaunchKernelGGL(k_pg_rollout_ws, dim3((unsigned)((n + kLsEnvs - 1) / kLsEnvs)), dim3(kWsThreads), 0,
+                           as_stream(stream), p);
+        if (int rc = launch_check("k_pg_rollout_ws")) return rc;
+        if (a->diag_flags & 128) {  // diagnostics: mean cycles per env per step segment, env / aux waves
+            std::vector<unsigned long long> h((size_t)n * 16);
+            (void)hipStreamSynchronize(as_stream(stream));
+            (void)hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost);
+            for (int w = 0; w < 2; ++w) {
+                fprintf(stderr, "rollout_ws %s cycles/step:", w ? "aux" : "env");
+                for (int k = 0; k < 7; ++k) {
+                    double sum = 0;
+                    for (int64_t e = 0; e < n; ++e) sum += (double)h[e * 16 + 8 * w + k];
+                    fprintf(stderr, " s%d=%.0f", k, sum / n / a->horizon);
+                }
+                fprintf(stderr, "\n");
+            }
+        }
+        return DXRL_OK;
+    }
     hipLaunchKernelGGL(k_pg_rollout_ls, dim3((unsigned)((n + kLsEnvs - 1) / kLsEnvs)), dim3(64 * kRolloutWaves), 0,
                        as_stream(stream), p);
     if (int rc = launch_check("k_pg_rollout_ls")) return rc;

@@ -14,7 +14,7 @@ for cur in ("easy", "hard"):
     tr = trainer.PGTrainer(env, trainer.TrainerConfig(horizon=200, seed=7))
     env.reset(write_obs=False)
     tr.rollout()
-    tr.diag_flags = 32
+    tr.diag_flags = int(os.environ.get("DIAG", "128"))
     print(cur, flush=True)
     tr.rollout()
     torch.cuda.synchronize()

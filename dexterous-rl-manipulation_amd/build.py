@@ -35,15 +35,29 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(f) <= t for f in _inputs())
 
 
-def build_native(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
-        return OUT
-    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
+ASAN_OUT = os.path.join(PKG_DIR, "libdxrl_asan.so")
+# host-side AddressSanitizer on the C-ABI shim (argument checks, handle / layout logic, error
+# plumbing); device code is compiled without it (GPU ASan is not available on this pool).  Load
+# with LD_PRELOAD=asan_runtime() and DXRL_LIB=ASAN_OUT (tests/test_native_abi.py does).
+ASAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer", "-g"]
+
+
+def asan_runtime() -> str:
+    import glob
+    hits = sorted(glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
+    return hits[-1] if hits else ""
+
+
+def build_native(force: bool = False, verbose: bool = False, asan: bool = False) -> str:
+    out = ASAN_OUT if asan else OUT
+    if not force and os.path.exists(out) and all(os.path.getmtime(f) <= os.path.getmtime(out) for f in _inputs()):
+        return out
+    cmd = [HIPCC, *FLAGS, *(ASAN_FLAGS if asan else []), "-o", out + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True, cwd=CSRC)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

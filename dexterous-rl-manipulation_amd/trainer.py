@@ -83,6 +83,14 @@ class TrainerConfig:
     success_rule: str = "terminated"         # "training" (episode_utils.py:52) or "terminated"
 
 
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 class PGTrainer:
     def __init__(self, env: VecEnv, cfg: TrainerConfig = TrainerConfig(), process_group=None, world_size: int = 1):
         if env.reward_type != "dense":
@@ -448,12 +456,15 @@ class PGTrainer:
         return rec
 
     def iteration(self, update: bool = True):
+        from . import profiling
+        marks = profiling.enabled()
         for name in self.phases():
-            if name == "ppo_updates" and not update:
-                self.actor_train()
-                self.critic_train()
-            elif name != "optimizer_step" or update:
-                getattr(self, name)()
+            with profiling.range_(f"pg.{name}") if marks else _null():
+                if name == "ppo_updates" and not update:
+                    self.actor_train()
+                    self.critic_train()
+                elif name != "optimizer_step" or update:
+                    getattr(self, name)()
         self.iteration_index += 1
 
     # ------------------------------------------------------------------ stats

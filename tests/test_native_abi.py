@@ -91,3 +91,24 @@ def test_ctypes_struct_layouts_match_c(native):
         assert int(got[s]) == C.sizeof(mirror[s]), s
         for f, _ in mirror[s]._fields_:
             assert int(got[f"{s}.{f}"]) == getattr(mirror[s], f).offset, f"{s}.{f}"
+
+
+def test_abi_checks_under_host_asan():
+    """The C-ABI shim's host code (argument validation, layout queries, error strings, the
+    struct-layout probe) under AddressSanitizer: this file's other tests re-run in a child
+    process against libdxrl_asan.so (host code built with -fsanitize=address, __graft_entry__
+    .build() builds it) with the clang ASan runtime preloaded.  Any ASan report fails the run."""
+    import os
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "dexterous-rl-manipulation_amd"))
+    import build as B
+    rt = B.asan_runtime()
+    if not rt or not os.path.exists(B.ASAN_OUT):
+        pytest.skip("libdxrl_asan.so not built (run __graft_entry__.build())")
+    env = dict(os.environ, LD_PRELOAD=rt, DXRL_LIB=B.ASAN_OUT, DXRL_ASAN_CHILD="1",
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:halt_on_error=1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", os.path.abspath(__file__),
+                        "-k", "not host_asan"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "AddressSanitizer" not in r.stderr, r.stdout[-2000:] + r.stderr[-2000:]

@@ -379,4 +379,105 @@ __device__ __forceinline__ void store_env(const EnvSoA& s, int64_t i, const Env&
     s.fric[i] = e.fric;
 }
 
+// standard normal k of Philox block k / 4 (Box-Muller pairs (x, y), (z, w)), as philox_normals
+__device__ __forceinline__ float philox_normal_at(int k, uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream) {
+    const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)(k >> 2)}, k0, k1);
+    float n0, n1;  // operands selected first: one branch-free Box-Muller (schedulable into MFMA gaps)
+    const bool hi = (k & 2) != 0;
+    box_muller(hi ? r.z : r.x, hi ? r.w : r.y, n0, n1);
+    return (k & 1) ? n1 : n0;
+}
+
+// 53-bit uniform of reset slot k (Philox block k / 2, half k % 2), as env_reset_philox
+__device__ __forceinline__ double reset_uniform_at(int k, uint32_t k0, uint32_t k1, uint64_t ctr) {
+    const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamReset, (uint32_t)(k >> 1)}, k0, k1);
+    return (k & 1) ? u01_53(r.z, r.w) : u01_53(r.x, r.y);
+}
+
+// ---------------------------------------------------------------- lane-split envs
+// An env spread over the 16 lanes of one DPP row (lane s: joint s, lanes 0..2 the object axes);
+// row_newbcast:K (DPP control 0x150 + K) hands lane K's value to every lane of its row in one
+// VALU op.  Used by the rollout (k_pg_rollout_ws) and the evaluation programs (k_eval_ls);
+// call only where the whole row is active.
+template <int K>
+__device__ __forceinline__ uint32_t row_bcast_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x150 + K, 0xF, 0xF, false);  // row_newbcast:K
+}
+template <int K>
+__device__ __forceinline__ float row_bcast(float x) {
+    return __uint_as_float(row_bcast_u32<K>(__float_as_uint(x)));
+}
+template <int K>
+__device__ __forceinline__ double row_bcast(double x) {
+    const uint64_t u = (uint64_t)__double_as_longlong(x);
+    const uint64_t lo = row_bcast_u32<K>((uint32_t)u), hi = row_bcast_u32<K>((uint32_t)(u >> 32));
+    return __longlong_as_double((long long)((hi << 32) | lo));
+}
+// acc = ((acc + x_0) + x_1) + ... + x_{N-1} with x_k = lane k's x (the reference's sequential order)
+template <int N, int K = 0>
+__device__ __forceinline__ void row_sum_in_order(float x, float& acc) {
+    if constexpr (K < N) {
+        acc += row_bcast<K>(x);
+        row_sum_in_order<N, K + 1>(x, acc);
+    }
+}
+template <int K = 0>
+__device__ __forceinline__ void row_joints(float jp, float (&J)[kD]) {
+    if constexpr (K < kD) {
+        J[K] = row_bcast<K>(jp);
+        row_joints<K + 1>(jp, J);
+    }
+}
+// Lane-split contacts_of (ME:285-310) over a DPP row: lane f < 5 computes finger f from the three
+// joint positions of lanes 3f..3f+2; every lane gets the mask (ballot) and the minimum distance.
+__device__ __forceinline__ uint32_t row_contacts(float jp, const double op[3], double size, int s, int gbit,
+                                                 double& dmin, float g3[3]) {
+    float J[kD];
+    row_joints(jp, J);
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+        float g = J[j];
+#pragma unroll
+        for (int f = 1; f < kF; ++f) g = s == f ? J[kJ * f + j] : g;
+        g3[j] = g;
+    }
+    float sum = g3[0];
+#pragma unroll
+    for (int j = 1; j < kJ; ++j) sum = sum + g3[j];
+    const double tip = (double)(sum * kC01);
+    const double dx = tip - op[0], dy = tip - op[1], dz = tip - op[2];
+    const double d = sqrt((dx * dx + dy * dy) + dz * dz);
+    const bool hit = s < kF && d < size * 1.5;
+    const uint32_t mask = (uint32_t)(__ballot(hit) >> gbit) & ((1u << kF) - 1u);
+    dmin = row_bcast<0>(d);
+    const double d1 = row_bcast<1>(d), d2 = row_bcast<2>(d), d3 = row_bcast<3>(d), d4 = row_bcast<4>(d);
+    dmin = d1 < dmin ? d1 : dmin;
+    dmin = d2 < dmin ? d2 : dmin;
+    dmin = d3 < dmin ? d3 : dmin;
+    dmin = d4 < dmin ? d4 : dmin;
+    return mask;
+}
+__device__ __forceinline__ void row_object(double opd, double op[3]) {
+    op[0] = row_bcast<0>(opd);
+    op[1] = row_bcast<1>(opd);
+    op[2] = row_bcast<2>(opd);
+}
+
+// acc = ((acc + (-x_0)) + (-x_1)) + ...  (the closure term's sum of finger sums, RS:147-162)
+template <int N, int K = 0>
+__device__ __forceinline__ void row_neg_sum_in_order(float x, float& acc) {
+    if constexpr (K < N) {
+        acc = acc + (-row_bcast<K>(x));
+        row_neg_sum_in_order<N, K + 1>(x, acc);
+    }
+}
+
+// observation element k written by lane s (ME:254-264), slot j of at most 4; -1 = none
+__device__ __forceinline__ int row_obs_elem(int s, int j) {
+    if (j == 0) return s < kD ? s : -1;
+    if (j == 1) return s < kD ? kD + s : -1;
+    if (j == 2) return s < 7 ? 2 * kD + s : (s < 7 + kF ? 2 * kD + 10 + (s - 7) : -1);
+    return s < 3 ? 2 * kD + 7 + s : -1;
+}
+
 }  // namespace dxrl

@@ -391,21 +391,6 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout(PgRolloutA
 // MFMA tile of which rows 0..15 are this workgroup's envs.
 constexpr int kLsEnvs = 16;  // 16 lanes per env: envs per workgroup = 256 threads / 16
 
-// standard normal k of Philox block k / 4 (Box-Muller pairs (x, y), (z, w)), as philox_normals
-__device__ __forceinline__ float philox_normal_at(int k, uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream) {
-    const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)(k >> 2)}, k0, k1);
-    float n0, n1;  // operands selected first: one branch-free Box-Muller (schedulable into MFMA gaps)
-    const bool hi = (k & 2) != 0;
-    box_muller(hi ? r.z : r.x, hi ? r.w : r.y, n0, n1);
-    return (k & 1) ? n1 : n0;
-}
-
-// 53-bit uniform of reset slot k (Philox block k / 2, half k % 2), as env_reset_philox
-__device__ __forceinline__ double reset_uniform_at(int k, uint32_t k0, uint32_t k1, uint64_t ctr) {
-    const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamReset, (uint32_t)(k >> 1)}, k0, k1);
-    return (k & 1) ? u01_53(r.z, r.w) : u01_53(r.x, r.y);
-}
-
 // In-group exchange through a per-env LDS row (dwords): one LDS write + wide reads replace a
 // chain of ds_bpermute shuffles.  All 16 lanes of a group are in one wave, so a wavefront-scope
 // fence (compiler ordering + lgkmcnt) is the only synchronisation needed.
@@ -836,82 +821,10 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-template <int K>
-__device__ __forceinline__ uint32_t row_bcast_u32(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x150 + K, 0xF, 0xF, false);  // row_newbcast:K
-}
-template <int K>
-__device__ __forceinline__ float row_bcast(float x) {
-    return __uint_as_float(row_bcast_u32<K>(__float_as_uint(x)));
-}
-template <int K>
-__device__ __forceinline__ double row_bcast(double x) {
-    const uint64_t u = (uint64_t)__double_as_longlong(x);
-    const uint64_t lo = row_bcast_u32<K>((uint32_t)u), hi = row_bcast_u32<K>((uint32_t)(u >> 32));
-    return __longlong_as_double((long long)((hi << 32) | lo));
-}
-// acc = ((acc + x_0) + x_1) + ... + x_{N-1} with x_k = lane k's x (the reference's sequential order)
-template <int N, int K = 0>
-__device__ __forceinline__ void row_sum_in_order(float x, float& acc) {
-    if constexpr (K < N) {
-        acc += row_bcast<K>(x);
-        row_sum_in_order<N, K + 1>(x, acc);
-    }
-}
-template <int K = 0>
-__device__ __forceinline__ void row_joints(float jp, float (&J)[kD]) {
-    if constexpr (K < kD) {
-        J[K] = row_bcast<K>(jp);
-        row_joints<K + 1>(jp, J);
-    }
-}
-// Lane-split contacts_of (ME:285-310) over a DPP row: lane f < 5 computes finger f from the three
-// joint positions of lanes 3f..3f+2; every lane gets the mask (ballot) and the minimum distance.
-__device__ __forceinline__ uint32_t row_contacts(float jp, const double op[3], double size, int s, int gbit,
-                                                 double& dmin, float g3[3]) {
-    float J[kD];
-    row_joints(jp, J);
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-        float g = J[j];
-#pragma unroll
-        for (int f = 1; f < kF; ++f) g = s == f ? J[kJ * f + j] : g;
-        g3[j] = g;
-    }
-    float sum = g3[0];
-#pragma unroll
-    for (int j = 1; j < kJ; ++j) sum = sum + g3[j];
-    const double tip = (double)(sum * kC01);
-    const double dx = tip - op[0], dy = tip - op[1], dz = tip - op[2];
-    const double d = sqrt((dx * dx + dy * dy) + dz * dz);
-    const bool hit = s < kF && d < size * 1.5;
-    const uint32_t mask = (uint32_t)(__ballot(hit) >> gbit) & ((1u << kF) - 1u);
-    dmin = row_bcast<0>(d);
-    const double d1 = row_bcast<1>(d), d2 = row_bcast<2>(d), d3 = row_bcast<3>(d), d4 = row_bcast<4>(d);
-    dmin = d1 < dmin ? d1 : dmin;
-    dmin = d2 < dmin ? d2 : dmin;
-    dmin = d3 < dmin ? d3 : dmin;
-    dmin = d4 < dmin ? d4 : dmin;
-    return mask;
-}
-__device__ __forceinline__ void row_object(double opd, double op[3]) {
-    op[0] = row_bcast<0>(opd);
-    op[1] = row_bcast<1>(opd);
-    op[2] = row_bcast<2>(opd);
-}
-
-// observation element k written by lane s (ME:254-264), slot j of at most 4; -1 = none
-__device__ __forceinline__ int ws_obs_elem(int s, int j) {
-    if (j == 0) return s < kD ? s : -1;
-    if (j == 1) return s < kD ? kD + s : -1;
-    if (j == 2) return s < 7 ? 2 * kD + s : (s < 7 + kF ? 2 * kD + 10 + (s - 7) : -1);
-    return s < 3 ? 2 * kD + 7 + s : -1;
-}
-
 // One env lane's draws, computed by its aux twin (structure of arrays over the 256 env lanes):
 // the action / dynamics noise normals and the reset uniforms (at the env's exact reset counter)
 // of the current step, and the observation-noise normals of the lane's obs elements
-// (ws_obs_elem) for the next observation row.  Single-buffered: each is written in the head
+// (row_obs_elem) for the next observation row.  Single-buffered: each is written in the head
 // phase and read before the next head phase.  The reward inputs (WsReward) are double-buffered
 // by step parity: the env lanes write step t's while the aux lanes settle step t-1's.
 struct WsDraws {
@@ -1046,7 +959,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     // dynamics-noise block s - 11 (normals 4(s-11) .. +3); lanes 0..11 observation-noise block s
     // (obs elements 4s .. 4s + 3).  Same blocks and arithmetic as philox_normal_at /
     // reset_uniform_at, so the values are identical.
-    const auto obs_slot = [&](int k, int& ln, int& j) {  // inverse of ws_obs_elem
+    const auto obs_slot = [&](int k, int& ln, int& j) {  // inverse of row_obs_elem
         if (k < kD) {
             ln = k;
             j = 0;
@@ -1156,7 +1069,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         bf16* xr = X + eg * kXs;
         const auto put = [&](int j, float v) {
             if (obs_noise) v = v + p.obs_noise * DR.on[j][et_tid];
-            xr[ws_obs_elem(s, j)] = to_bf16(v);
+            xr[row_obs_elem(s, j)] = to_bf16(v);
         };
         if (s < kD) {
             put(0, jp);

@@ -248,3 +248,34 @@ def test_host_policy_runs_through_facade():
     for got, want in zip(rob["episodes"], g["robustness"]):
         check_episode(got, want, with_props=False)
     close_dict(rob["metrics"], g["robustness_metrics"])
+
+
+@pytest.mark.parametrize("policy,noise,traj", [("simple", (0.0, 0.0), False), ("heuristic", (0.05, 0.1), True),
+                                               ("random", (0.0, 0.3), False)])
+def test_lane_split_eval_matches_one_lane_kernel(policy, noise, traj, monkeypatch):
+    """k_eval_ls (16 lanes per env, rows fed from a work queue; the default) == k_eval (one lane
+    per chain, DXRL_EVAL_ONE_LANE=1) bit for bit in the device-stream form (Philox policy, noise
+    and reset streams), including trajectories, contact histories and multi-segment lanes."""
+    rng = np.random.default_rng(7)
+    configs = [cfg_of("variable"), cfg_of("hard"), cfg_of("easy")]
+    pol = make_policy(policy, rng.uniform(-0.5, 0.5, 15).astype(np.float32), 3)
+    prog = evr.policy_program(pol)
+    p = evr.EpisodeProgram(configs, "dense", max_episode_steps=120, max_steps=100)
+    for lane in range(300):
+        segs = []
+        for _ in range(int(rng.integers(1, 3))):
+            o, d = noise if rng.random() < 0.5 else (0.0, 0.0)
+            segs.append(evr.Segment(int(rng.integers(0, 3)), [int(x) for x in rng.integers(0, 10**6, rng.integers(1, 3))],
+                                    o, d, noise_seed=int(rng.integers(0, 10**6))))
+        p.add_lane(segs)
+    out = []
+    for one in ("1", "0"):
+        monkeypatch.setenv("DXRL_EVAL_ONE_LANE", one)
+        out.append(p.run(prog, host_resets=False, host_noise=False, trajectories=traj))
+    a, b = out
+    for k in ("ep_return", "ep_length", "ep_success", "ep_contacts", "contact_hist", "policy_used"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    if traj:  # rows past an episode's end are untouched by the kernels: compare the written ones
+        for i, n in enumerate(a.ep_length.astype(int)):
+            assert np.array_equal(a.obs_traj[i, :n + 1], b.obs_traj[i, :n + 1]), i
+            assert np.array_equal(a.act_traj[i, :n], b.act_traj[i, :n]), i

@@ -18,6 +18,31 @@ class Frozen:
     mean_action = np.asarray(MEAN, np.float32)
 
 
+def measured_efficiency(p, prog, steps, hist):
+    """One diagnostic launch (DXRL_EVAL_DIAG=1): the kernel reports the step iterations its waves
+    executed; each iteration of a 64-lane wave offers 4 env-step slots (k_eval_ls: 16 lanes per
+    env) or 64 (the one-lane kernel).  Efficiency = env steps / slots."""
+    import os
+    import tempfile
+    one = os.environ.get("DXRL_EVAL_ONE_LANE", "0") not in ("", "0")
+    if one:
+        return None
+    os.environ["DXRL_EVAL_DIAG"] = "1"
+    with tempfile.TemporaryFile(mode="w+") as f:
+        saved = os.dup(2)
+        os.dup2(f.fileno(), 2)
+        try:
+            p.run(prog, host_resets=False, host_noise=False, keep_history=hist)
+        finally:
+            os.dup2(saved, 2)
+            os.close(saved)
+            del os.environ["DXRL_EVAL_DIAG"]
+        f.seek(0)
+        line = [x for x in f.read().splitlines() if "wave_iterations=" in x][-1]
+    it = int(line.split("wave_iterations=")[1].split()[0])
+    return steps / (4 * it)
+
+
 def wave_steps(lengths):
     """Lane-steps the waves execute: every lane of a 64-lane wave runs as long as its longest episode."""
     L = np.zeros(-(-len(lengths) // 64) * 64, np.int64)
@@ -44,7 +69,8 @@ def main():
                           "episodes": E, "env_steps": steps, "mean_length": steps / E,
                           "kernel_ms": round(t["kernel_ms"], 4), "episodes_per_s": E / (t["kernel_ms"] * 1e-3),
                           "env_steps_per_s": steps / (t["kernel_ms"] * 1e-3),
-                          "wave_efficiency": steps / wave_steps(rec.ep_length),
+                          "wave_efficiency_one_lane_model": steps / wave_steps(rec.ep_length),
+                          "wave_efficiency_measured": measured_efficiency(p, prog, steps, hist),
                           "success_rate": float(rec.ep_success.mean()), "host_wall_s_20_launches": wall}))
 
 

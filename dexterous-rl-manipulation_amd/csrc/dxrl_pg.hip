@@ -155,10 +155,13 @@ __device__ __forceinline__ void load_wtile(WTile<KS>& w, const bf16* W, int ldw,
 
 // One wave: 64 rows x 32*NT columns of act(A . W^T + b) into LDS.  A: LDS [64][lda]
 // bf16; the weight fragment of N-tile j, k-step k comes from wfrag(j, k) (registers
-// or LDS); bias: f32 master column (bias[n * ldb]), the values the training GEMMs use.
+// or LDS); bias: f32 master column (bias[n * ldb]), the values the training GEMMs use, or
+// bias_v[j] = that value already in a register (a persistent kernel hoists the load: a global
+// load inside the step loop puts a vmcnt(0) -- which also drains every outstanding tape store --
+// on the step's critical path).
 template <int KS, int NT, bool kTanh, int RT = 2, typename WF>
 __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfrag, int n0, const float* bias_p,
-                                           int ldb, bf16* out, int ldo, int lane) {
+                                           int ldb, bf16* out, int ldo, int lane, const float* bias_v = nullptr) {
     // RT row tiles of 32 (RT == 1: 16 live rows -- accumulator registers q < 8)
     constexpr int kQ = RT == 1 ? 8 : 16;
     const int r = lane & 31, h = lane >> 5;
@@ -196,7 +199,7 @@ __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfr
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         const int n = n0 + 32 * j + r;
-        const float bias = bias_p ? bias_p[(int64_t)n * ldb] : 0.0f;
+        const float bias = bias_v ? bias_v[j] : bias_p ? bias_p[(int64_t)n * ldb] : 0.0f;
         const float bk = tanh_bias(bias);
 #pragma unroll
         for (int i = 0; i < RT; ++i)
@@ -900,6 +903,9 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         return *reinterpret_cast<const bf16x8*>(W1s + (32 * wave + r32) * kW1s + 16 * k + 8 * h2);
     };
     const auto w2frag = [&](int, int k) { return w2.b[k]; };
+    // step-invariant biases in registers: L2 column 32 wave + r32, head row r32
+    const float b2_reg = p.params[kOffW2a + (int64_t)(32 * wave + r32) * kHx + kH];
+    const float b3_reg = p.params[kOffW3a + (int64_t)r32 * kHx + kH];
 
     // ---- env-lane state (env waves) / episode bookkeeping (aux waves)
     float jp = 0.0f, jv = 0.0f;
@@ -1226,8 +1232,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         if (mlp) wave_layer<kIn / 16, 1, true, 1>(X, kXs, w1frag, 32 * wave, nullptr, 0, H1, kHs, lane);
         WS_STAMP(1);
         lds_barrier();
-        if (mlp)
-            wave_layer<kH / 16, 1, true, 1>(H1, kHs, w2frag, 32 * wave, p.params + kOffW2a + kH, kHx, H2, kHs, lane);
+        if (mlp) wave_layer<kH / 16, 1, true, 1>(H1, kHs, w2frag, 32 * wave, nullptr, 0, H2, kHs, lane, &b2_reg);
         WS_STAMP(2);
         lds_barrier();
         if (mlp && wave == kHeadWave) {  // mu head: 16 env rows x 32 head rows
@@ -1246,9 +1251,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
 #pragma unroll
                 for (int k = 0; k < 4; ++k) acc = mfma32(ah[k], bw[k], acc);
             }
-            const float bias = p.params[kOffW3a + (int64_t)r32 * kHx + kH];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) MU[acc_row(q, lane) * (kOut + 1) + r32] = acc[q] + bias;  // rows < 16
+            for (int q = 0; q < 8; ++q) MU[acc_row(q, lane) * (kOut + 1) + r32] = acc[q] + b3_reg;  // rows < 16
         }
         if (aux && live) {
             // this step's draws at the reset counter it sees (step t-1's episode end is known:

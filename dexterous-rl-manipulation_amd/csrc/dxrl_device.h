@@ -47,8 +47,10 @@ struct u32x4 {
 __device__ __forceinline__ u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        // each 32x32 -> 64-bit product as one v_mad_u64_u32 (both halves), not mul_lo + mul_hi
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;

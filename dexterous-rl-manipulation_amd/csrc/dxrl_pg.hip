@@ -159,7 +159,7 @@ __device__ __forceinline__ void load_wtile(WTile<KS>& w, const bf16* W, int ldw,
 // bias_v[j] = that value already in a register (a persistent kernel hoists the load: a global
 // load inside the step loop puts a vmcnt(0) -- which also drains every outstanding tape store --
 // on the step's critical path).
-template <int KS, int NT, bool kTanh, int RT = 2, typename WF>
+template <int KS, int NT, bool kTanh, int RT = 2, typename WF, bool kRing = false>
 __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfrag, int n0, const float* bias_p,
                                            int ldb, bf16* out, int ldo, int lane, const float* bias_v = nullptr) {
     // RT row tiles of 32 (RT == 1: 16 live rows -- accumulator registers q < 8)
@@ -172,7 +172,7 @@ __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfr
         for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.0f;
-    if constexpr (RT == 1) {
+    if constexpr (RT == 1 && !kRing) {
         // one row tile: issue every activation fragment up front (KS LDS reads in flight),
         // then the MFMA chain consumes them with counted waits
         bf16x8 a[KS];
@@ -182,6 +182,23 @@ __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfr
         for (int k = 0; k < KS; ++k)
 #pragma unroll
             for (int j = 0; j < NT; ++j) acc[0][j] = mfma32(a[k], wfrag(j, k), acc[0][j]);
+    } else if constexpr (RT == 1) {
+        // one row tile: a ring of kD activation fragments, refilled kD k-steps ahead; the
+        // scheduling barriers keep the refills where they are (under register pressure the
+        // scheduler otherwise sinks every read next to its MFMA, exposing one LDS latency per
+        // k-step instead of one per chain)
+        constexpr int kD = KS < 4 ? KS : 4;
+        bf16x8 a[kD];
+#pragma unroll
+        for (int k = 0; k < kD; ++k) a[k] = *reinterpret_cast<const bf16x8*>(A + r * lda + 16 * k + 8 * h);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[0][j] = mfma32(a[k % kD], wfrag(j, k), acc[0][j]);
+            if (k + kD < KS) a[k % kD] = *reinterpret_cast<const bf16x8*>(A + r * lda + 16 * (k + kD) + 8 * h);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
@@ -834,23 +851,29 @@ struct WsDraws {
     float eps[256], dzn[256], on[4][256];
     double u1[256], u2[256];
 };
+struct WsSampler {     // one env lane's extra reset draw: has ? lo + span u : cst
+    double lo, span, cst;
+    int32_t has, pad;
+};
 struct WsReward {      // an env's dense-reward inputs and episode end of one step
     double dmin;
     uint32_t c, prev;  // contacts, previous contacts (0x100: none)
     float nacc[kF];    // per finger: sum of its negative joint positions
     int32_t len;       // episode length after the step
     int32_t done, te;
+    unsigned long long rctr;  // reset counter after the step (the next step's reset draws use it)
 };
 
 // Step t of a workgroup (16 envs, 8 waves):
 //   P0  env lanes write the observation row (+ observation noise drawn in step t-1's P3)
 //   P1  all waves: L1, one 32-column tile each            (the env lanes also store the obs row)
 //   P2  all waves: L2, one 32-column tile each
-//   P3  env wave 3: the mu head.  Aux lanes, in that shadow: settle step t-1's reward and
-//       bookkeeping, then draw step t's action / dynamics noise and reset uniforms (the reset
-//       counter is exact now: step t-1's episode end is known) and step t+1's observation noise
+//   P3  env wave 3: the mu head.  In its shadow, one drawing wave per SIMD (step_draws): wave 0
+//       step t's action noise, waves 1, 2, 7 the reset uniforms at each env's exact counter (step
+//       t-1's episode end is known); aux lanes: step t+1's observation noise
 //   P4  env lanes: a = mu + sigma eps, dynamics, contacts, termination, auto-reset.
-//       Aux lanes: the same a, log pi (DPP row sum in action order), the act / log pi tape
+//       Aux lanes: the same a, log pi (DPP row sum in action order), the act / log pi tape, then
+//       settle step t-1's reward and episode bookkeeping
 __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p) {
     constexpr int kRows = 32;
     constexpr int kHeadWave = 3;  // an env wave: the env lanes idle while the head runs
@@ -863,6 +886,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     __shared__ float LS[kActPad], SIG[kActPad], ISIG[kActPad];
     __shared__ WsDraws DR;
     __shared__ WsReward RW[2][kLsEnvs];
+    __shared__ WsSampler RSMP[kWsThreads / 2];
+    __shared__ uint32_t KEYS[kLsEnvs][4];           // per env: reset key ek0, ek1, policy key pk0, pk1
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool aux = wave >= 4;
     const int et_tid = tid & 255;  // the env lane this thread is (env wave) or twins (aux wave)
@@ -941,6 +966,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         env_key(p.policy_seed, p.gid0 + i, pk0, pk1);
     }
     const int s2 = s < DXRL_RESET_EXTRA ? s : 0;
+    // this lane's extra reset sampler (config.py:44-113) -- read only when an episode ends, so
+    // kept in LDS rather than in registers: RSMP[et_tid] = {lo, hi - lo, constant, has range}
     double lo2 = 0.0, hi2 = 0.0, cst2 = 0.0;
     bool has2 = true, fric64 = false;
     if (live && !aux) {
@@ -953,10 +980,18 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         hi2 = rg[1];
         cst2 = s2 == 0 ? cu.object_size : s2 == 1 ? cu.object_mass : cu.friction_coefficient;
         has2 = s2 == 0 ? cu.has_size_range != 0 : s2 == 1 ? cu.has_mass_range != 0 : s2 == 2 ? cu.has_friction_range != 0 : true;
+        RSMP[et_tid] = WsSampler{lo2, hi2 - lo2, cst2, has2 ? 1 : 0};
         fric64 = cu.friction_is_f64_scalar != 0;
     }
     const int sa = s < kAct ? s : 0;
     const bool obs_noise = p.obs_noise > 0.0f, dyn_noise = p.dyn_noise > 0.0f;
+    if (live && !aux && s == 0) {
+        KEYS[eg][0] = ek0;
+        KEYS[eg][1] = ek1;
+        KEYS[eg][2] = pk0;
+        KEYS[eg][3] = pk1;
+        RW[1][eg].rctr = rctr;  // "after step -1"
+    }
 
     // ---- aux: Philox draws.  Each block is computed once per env row and its values written
     // straight into the LDS slots of the env lanes that use them (k_pg_rollout_ls recomputes the
@@ -988,37 +1023,48 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         box_muller(r.x, r.y, nz[0], nz[1]);
         box_muller(r.z, r.w, nz[2], nz[3]);
     };
+    // Step t's action / dynamics noise and reset uniforms, computed in the head phase by waves
+    // that each have a SIMD to themselves for it (waves w and w + 4 share SIMD w; Philox's 64-bit
+    // products are quarter-rate, so two drawing waves on one SIMD serialise): one Philox block per
+    // lane, keys (KEYS) and reset counters (RW[.].rctr) of all 16 envs from LDS, values written
+    // straight into the consumers' slots.
+    //   wave 0 (SIMD 0)        action noise: lane -> (env lane >> 2, block lane & 3)
+    //   waves 1, 2, 7 (SIMD 1, 2, 3 -- 3 runs the head on the matrix core): group lane g < 176
+    //                          reset block g % 11 of env g / 11 (u01_53 of both halves: joint
+    //                          slots 0..14 -> u1, extra slots 15..20 -> u2)
+    //   wave 4 (SIMD 0)        dynamics noise (robustness configs only), as wave 0
     constexpr int kResetBlocks = (kReset + 1) / 2;
-    const auto step_draws = [&](uint64_t ctr, uint64_t rc) {  // step ctr's noise, reset at counter rc
-        // one Philox call for the whole wave (lanes 0..10 a reset block, 11..14 an action-noise
-        // block), then per-lane conversion and scatter
-        const bool rs = s < kResetBlocks;
-        const int blk = rs ? s : s - kResetBlocks;
-        const uint64_t c = rs ? rc : ctr;
-        const u32x4 r = philox(u32x4{(uint32_t)c, (uint32_t)(c >> 32), rs ? kStreamReset : kStreamPolicy, (uint32_t)blk},
-                               rs ? ek0 : pk0, rs ? ek1 : pk1);
-        if (rs) {
-            const double ua = u01_53(r.x, r.y), ub = u01_53(r.z, r.w);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int k = 2 * s + h;
-                const double u = h ? ub : ua;
-                if (k < kD) DR.u1[rbase + k] = u;
-                else if (k < kReset) DR.u2[rbase + k - kD] = u;
-            }
-        } else if (blk < 4) {
+    const auto step_draws = [&](uint64_t ctr, int64_t t_) {
+        if (wave == 0 || (wave == 4 && dyn_noise)) {
+            const int e = lane >> 2, blk = lane & 3;
+            if ((int64_t)blockIdx.x * kLsEnvs + e >= n) return;
+            const uint32_t stream = wave == 0 ? kStreamPolicy : kStreamDyn;
+            const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)blk},
+                                   KEYS[e][2], KEYS[e][3]);
             float nz[4];
             box_muller(r.x, r.y, nz[0], nz[1]);
             box_muller(r.z, r.w, nz[2], nz[3]);
+            float* dst = wave == 0 ? DR.eps : DR.dzn;
 #pragma unroll
             for (int h = 0; h < 4; ++h)
-                if (4 * blk + h < kAct) DR.eps[rbase + 4 * blk + h] = nz[h];
-            if (dyn_noise) {
-                normals4(ctr, kStreamDyn, blk, nz);
+                if (4 * blk + h < kAct) dst[16 * e + 4 * blk + h] = nz[h];
+            return;
+        }
+        if (wave != 1 && wave != 2 && wave != 7) return;
+        const int g = 64 * (wave == 7 ? 2 : wave - 1) + lane;
+        if (g >= kLsEnvs * kResetBlocks) return;
+        const int e = g / kResetBlocks, blk = g % kResetBlocks;
+        if ((int64_t)blockIdx.x * kLsEnvs + e >= n) return;
+        const uint64_t rc = RW[(t_ - 1) & 1][e].rctr;
+        const u32x4 r = philox(u32x4{(uint32_t)rc, (uint32_t)(rc >> 32), kStreamReset, (uint32_t)blk},
+                               KEYS[e][0], KEYS[e][1]);
+        const double ua = u01_53(r.x, r.y), ub = u01_53(r.z, r.w);
 #pragma unroll
-                for (int h = 0; h < 4; ++h)
-                    if (4 * blk + h < kAct) DR.dzn[rbase + 4 * blk + h] = nz[h];
-            }
+        for (int h = 0; h < 2; ++h) {
+            const int k = 2 * blk + h;
+            const double u = h ? ub : ua;
+            if (k < kD) DR.u1[16 * e + k] = u;
+            else if (k < kReset) DR.u2[16 * e + k - kD] = u;
         }
     };
     const auto obs_draws = [&](uint64_t ctr) {  // the observation noise of row ctr
@@ -1162,7 +1208,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         if (d) {
             // ---- env_reset_philox, lane-split: lane s holds slot s (joint) and slot 15 + s
             const double u1 = DR.u1[et_tid], u2 = DR.u2[et_tid];
-            const double v2 = has2 ? lo2 + (hi2 - lo2) * u2 : cst2;  // config.py:44-113 samplers
+            const WsSampler sm = RSMP[et_tid];
+            const double v2 = sm.has ? sm.lo + sm.span * u2 : sm.cst;  // config.py:44-113 samplers
             if (s < kD) {
                 jp = (float)(-0.1 + (0.1 - -0.1) * u1);
                 jv = 0.0f;
@@ -1186,6 +1233,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             flags |= row_contacts(jp, op3, size, s, gbit, dmin, g3);
             ++rctr;
         }
+        if (s == 0) RW[t & 1][eg].rctr = rctr;
     };
     // ---- aux lanes, P4 of step t: the policy sample, log pi(a|s) (gauss_logp's order), tapes
     const auto aux_lane_step = [&](int64_t m) {
@@ -1232,34 +1280,42 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         if (mlp) wave_layer<kIn / 16, 1, true, 1>(X, kXs, w1frag, 32 * wave, nullptr, 0, H1, kHs, lane);
         WS_STAMP(1);
         lds_barrier();
-        if (mlp) wave_layer<kH / 16, 1, true, 1>(H1, kHs, w2frag, 32 * wave, nullptr, 0, H2, kHs, lane, &b2_reg);
+        if (mlp)
+            wave_layer<kH / 16, 1, true, 1, decltype(w2frag), true>(H1, kHs, w2frag, 32 * wave, nullptr, 0, H2, kHs, lane,
+                                                                    &b2_reg);
         WS_STAMP(2);
         lds_barrier();
         if (mlp && wave == kHeadWave) {  // mu head: 16 env rows x 32 head rows
             f32x16 acc;
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-            // H2 rows and W3 rows (head outputs) from LDS, 4 k-steps of fragments in flight
+            // H2 rows and W3 rows (head outputs) from LDS: a ring of 4 k-steps of fragments,
+            // refilled 4 ahead (pinned by scheduling barriers, as in wave_layer)
+            constexpr int kD = 4;
+            bf16x8 ah[kD], bw[kD];
 #pragma unroll
-            for (int k0 = 0; k0 < kH / 16; k0 += 4) {
-                bf16x8 ah[4], bw[4];
+            for (int k = 0; k < kD; ++k) {
+                ah[k] = *reinterpret_cast<const bf16x8*>(H2 + r32 * kHs + 16 * k + 8 * h2);
+                bw[k] = *reinterpret_cast<const bf16x8*>(W3s + r32 * kW3s + 16 * k + 8 * h2);
+            }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    ah[k] = *reinterpret_cast<const bf16x8*>(H2 + r32 * kHs + 16 * (k0 + k) + 8 * h2);
-                    bw[k] = *reinterpret_cast<const bf16x8*>(W3s + r32 * kW3s + 16 * (k0 + k) + 8 * h2);
+            for (int k = 0; k < kH / 16; ++k) {
+                acc = mfma32(ah[k % kD], bw[k % kD], acc);
+                if (k + kD < kH / 16) {
+                    ah[k % kD] = *reinterpret_cast<const bf16x8*>(H2 + r32 * kHs + 16 * (k + kD) + 8 * h2);
+                    bw[k % kD] = *reinterpret_cast<const bf16x8*>(W3s + r32 * kW3s + 16 * (k + kD) + 8 * h2);
                 }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) acc = mfma32(ah[k], bw[k], acc);
+                __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) MU[acc_row(q, lane) * (kOut + 1) + r32] = acc[q] + b3_reg;  // rows < 16
         }
-        if (aux && live) {
-            // this step's draws at the reset counter it sees (step t-1's episode end is known:
-            // its inputs were left before the last barriers), the next observation row's noise
-            if (t > 0 && env_on && RW[(t - 1) & 1][eg].done) ++rctr;
-            step_draws(ctr, rctr);
-            obs_draws(ctr + 1);
+        if (!(p.diag & 256)) {
+            // this step's draws (RW[(t - 1) & 1].rctr: the counters after step t-1's resets), the next
+            // observation row's noise (aux lanes, own rows)
+            if (wave != kHeadWave) step_draws(ctr, t);
+            if (aux && live) obs_draws(ctr + 1);
         }
         WS_STAMP(3);
         lds_barrier();
@@ -1267,7 +1323,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         if (live) {
             if (aux) {
                 aux_lane_step(m);
-                if (t > 0 && env_on) settle(t - 1);  // step t-1's reward and bookkeeping
+                if (t > 0 && env_on && !(p.diag & 512)) settle(t - 1);  // step t-1's reward and bookkeeping
             } else {
                 env_lane_step(t, m);
             }
@@ -1748,6 +1804,20 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                     fprintf(stderr, " s%d=%.0f", k, sum / n / a->horizon);
                 }
                 fprintf(stderr, "\n");
+                for (int wv = 0; wv < 4; ++wv) {  // per wave of the workgroup (envs 4 wv .. 4 wv + 3)
+                    fprintf(stderr, "  wave %d:", 4 * w + wv);
+                    for (int k = 0; k < 7; ++k) {
+                        double sum = 0;
+                        int64_t cnt = 0;
+                        for (int64_t e = 0; e < n; ++e)
+                            if ((e % kLsEnvs) / 4 == wv) {
+                                sum += (double)h[e * 16 + 8 * w + k];
+                                ++cnt;
+                            }
+                        fprintf(stderr, " s%d=%.0f", k, cnt ? sum / cnt / a->horizon : 0.0);
+                    }
+                    fprintf(stderr, "\n");
+                }
             }
         }
         return DXRL_OK;

@@ -13,7 +13,8 @@ for cur in ("easy", "hard"):
     env = envs.VecEnv(4096, curriculum_config=pkg.CurriculumConfig.named(cur), reward_type="dense", seed=1, device=dev)
     tr = trainer.PGTrainer(env, trainer.TrainerConfig(horizon=200, seed=7))
     env.reset(write_obs=False)
-    for flags, name in ((0, "ws full"), (1, "ws no-MLP"), (2, "ws no-env"), (3, "ws neither"), (64, "ls full"),
+    for flags, name in ((0, "ws full"), (1, "ws no-MLP"), (2, "ws no-env"), (3, "ws neither"), (256, "ws no-draws"),
+                        (512, "ws no-settle"), (768, "ws no-draws/settle"), (64, "ls full"),
                         (65, "ls no-MLP"), (66, "ls no-env"), (67, "ls neither")):
         tr.diag_flags = flags
         tr.rollout()
@@ -24,4 +25,4 @@ for cur in ("easy", "hard"):
             tr.rollout()
         b.record()
         torch.cuda.synchronize()
-        print(f"{cur:5s} {name:8s} {a.elapsed_time(b) / 5:8.3f} ms")
+        print(f"{cur:5s} {name:18s} {a.elapsed_time(b) / 5:8.3f} ms")

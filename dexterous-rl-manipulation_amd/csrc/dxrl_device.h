@@ -114,11 +114,26 @@ __device__ __forceinline__ uint32_t contacts_of(const Env& e, double& dmin) {
     return mask;
 }
 
+// k / kF for a contact count k = 0..kF, bit for bit the correctly rounded quotient (the quotients
+// are compile-time constants, selected: no division instruction sequence on the step's path)
+__device__ __forceinline__ double count_over_f_f64(uint32_t k) {
+    double r = 0.0;
+#pragma unroll
+    for (int q = 1; q <= kF; ++q) r = k == (uint32_t)q ? (double)q / (double)kF : r;
+    return r;
+}
+__device__ __forceinline__ float count_over_f_f32(uint32_t k) {
+    float r = 0.0f;
+#pragma unroll
+    for (int q = 1; q <= kF; ++q) r = k == (uint32_t)q ? (float)q / (float)kF : r;
+    return r;
+}
+
 // RS:101-187 dense terms + weighted total (RS:84-89); updates prev contacts.
 __device__ __forceinline__ double dense_reward(Env& e, uint32_t c, double dmin, const Weights& w, double comp[4]) {
     const double dist = exp(-5.0 * dmin);                 // RS:111-116
     const int n = __popc(c);
-    const double con = (double)n / (double)kF;            // RS:128-134
+    const double con = count_over_f_f64((uint32_t)n);     // RS:128-134 (n / 5)
     float sum = 0.0f;                                     // RS:147-162
 #pragma unroll
     for (int f = 0; f < kF; ++f) {
@@ -138,7 +153,7 @@ __device__ __forceinline__ double dense_reward(Env& e, uint32_t c, double dmin, 
         float ch = 0.0f;
 #pragma unroll
         for (int f = 0; f < kF; ++f) ch = ch + (float)(((c ^ prev) >> f) & 1u);
-        st = clipf(1.0f - ch / (float)kF, 0.0f, 1.0f);
+        st = clipf(1.0f - count_over_f_f32((uint32_t)ch), 0.0f, 1.0f);
     }
     e.flags = (e.flags & ~(0xFFu << kPrevShift)) | (c << kPrevShift) | kHasPrev;
     comp[0] = dist;
@@ -434,15 +449,12 @@ __device__ __forceinline__ void row_joints(float jp, float (&J)[kD]) {
 // joint positions of lanes 3f..3f+2; every lane gets the mask (ballot) and the minimum distance.
 __device__ __forceinline__ uint32_t row_contacts(float jp, const double op[3], double size, int s, int gbit,
                                                  double& dmin, float g3[3]) {
-    float J[kD];
-    row_joints(jp, J);
+    // finger s's joints (lanes 3s .. 3s + 2 of the row; lanes s >= kF take finger 0's) through the
+    // LDS crossbar: three ds_bpermute instead of 15 row broadcasts and 12 selects on the VALU
+    const int src = gbit + (s < kF ? kJ * s : 0);
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-        float g = J[j];
-#pragma unroll
-        for (int f = 1; f < kF; ++f) g = s == f ? J[kJ * f + j] : g;
-        g3[j] = g;
-    }
+    for (int j = 0; j < kJ; ++j)
+        g3[j] = __int_as_float(__builtin_amdgcn_ds_bpermute((src + j) << 2, __float_as_int(jp)));
     float sum = g3[0];
 #pragma unroll
     for (int j = 1; j < kJ; ++j) sum = sum + g3[j];

@@ -547,7 +547,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_ls(const dxrl_curriculum*
         double r;
         if (p.dense) {  // RS:50-187
             const double dist = exp(-5.0 * dmin);
-            const double con = (double)__popc(c) / (double)kF;
+            const double con = count_over_f_f64(__popc(c));
             float nacc = 0.0f;
 #pragma unroll
             for (int j = 0; j < kJ; ++j)
@@ -562,7 +562,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_ls(const dxrl_curriculum*
                 float ch = 0.0f;
 #pragma unroll
                 for (int f = 0; f < kF; ++f) ch = ch + (float)(((c ^ prev) >> f) & 1u);
-                st = clipf(1.0f - ch / (float)kF, 0.0f, 1.0f);
+                st = clipf(1.0f - count_over_f_f32((uint32_t)ch), 0.0f, 1.0f);
             }
             flags = (flags & ~(0xFFu << kPrevShift)) | (c << kPrevShift) | kHasPrev;
             r = ((p.w.w_dist * dist + p.w.w_con * con) + p.w.w_clo * (double)clo) + p.w.w_st * (double)st;

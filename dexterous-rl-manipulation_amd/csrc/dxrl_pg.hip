@@ -700,7 +700,7 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
             const uint32_t c = ls_contacts(jp, op3, size, s, gbit, dmin, g3, gx);
             // dense_reward (RS:101-187)
             const double dist = exp(-5.0 * dmin);
-            const double con = (double)__popc(c) / (double)kF;
+            const double con = count_over_f_f64(__popc(c));
             float nacc = 0.0f;  // finger s: sum of its negative joint positions
 #pragma unroll
             for (int j = 0; j < kJ; ++j)
@@ -718,7 +718,7 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
                 float ch = 0.0f;
 #pragma unroll
                 for (int f = 0; f < kF; ++f) ch = ch + (float)(((c ^ prev) >> f) & 1u);
-                st = clipf(1.0f - ch / (float)kF, 0.0f, 1.0f);
+                st = clipf(1.0f - count_over_f_f32((uint32_t)ch), 0.0f, 1.0f);
             }
             flags = (flags & ~(0xFFu << kPrevShift)) | (c << kPrevShift) | kHasPrev;
             r = ((p.w.w_dist * dist + p.w.w_con * con) + p.w.w_clo * (double)clo) + p.w.w_st * (double)st;
@@ -1035,6 +1035,11 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     //   wave 4 (SIMD 0)        dynamics noise (robustness configs only), as wave 0
     constexpr int kResetBlocks = (kReset + 1) / 2;
     const auto step_draws = [&](uint64_t ctr, int64_t t_) {
+        // the lane id re-read each step (volatile): the task indices and LDS addresses derived
+        // from it are then not hoisted out of the step loop, where they only raise register
+        // pressure into spills (each reload a vmcnt(0))
+        int lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
         if (wave == 0 || (wave == 4 && dyn_noise)) {
             const int e = lane >> 2, blk = lane & 3;
             if ((int64_t)blockIdx.x * kLsEnvs + e >= n) return;
@@ -1086,7 +1091,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     const auto settle = [&](int64_t t_) {
         const WsReward& w = RW[t_ & 1][eg];
         const double dist = exp(-5.0 * w.dmin);
-        const double con = (double)__popc(w.c) / (double)kF;
+        const double con = count_over_f_f64(__popc(w.c));
         float sum = 0.0f;
 #pragma unroll
         for (int f = 0; f < kF; ++f) sum = sum + (-w.nacc[f]);
@@ -1097,7 +1102,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             float ch = 0.0f;
 #pragma unroll
             for (int f = 0; f < kF; ++f) ch = ch + (float)(((w.c ^ w.prev) >> f) & 1u);
-            st = clipf(1.0f - ch / (float)kF, 0.0f, 1.0f);
+            st = clipf(1.0f - count_over_f_f32((uint32_t)ch), 0.0f, 1.0f);
         }
         const double r = ((p.w.w_dist * dist + p.w.w_con * con) + p.w.w_clo * (double)clo) + p.w.w_st * (double)st;
         ep_ret += r;

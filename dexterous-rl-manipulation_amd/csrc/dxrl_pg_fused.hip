@@ -372,8 +372,14 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     float db2 = 0.0f;  // threads < 256: dL/db2 of column tid
     float lsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // per-thread sums over <= ~25 tiles (f64 across threads)
 
-    const double adv_mean = kTrain && p.net == 0 ? p.stats[2] : 0.0;
-    const double adv_div = kTrain && p.net == 0 ? p.stats[4] + 1e-8 : 1.0;
+    // workgroup-uniform: pinned to scalar registers (as VGPR pairs they were spilled across the tile loop)
+    const auto uniform_f64 = [](double v) {
+        const uint64_t u = __double_as_longlong(v);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+        return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+    };
+    const double adv_mean = uniform_f64(kTrain && p.net == 0 ? p.stats[2] : 0.0);
+    const double adv_div = uniform_f64(kTrain && p.net == 0 ? p.stats[4] + 1e-8 : 1.0);
 
     // X tile prefetch: 128 rows x 8 chunks of 16 B = 1024 chunks, 4 per thread
     constexpr int kXU = kTR * (kIn / 8) / kFThreads;
@@ -448,7 +454,10 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         const int64_t m = m0 + ml;
         const bool valid = m < p.rows;
         float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
-        float lo = 0.0f, adv = 0.0f, ret = 0.0f;
+        // hv: the head's per-sample target -- old log pi (actor) or return (critic); one variable,
+        // not two assigned on the two net branches (the compiler merged those stores into one
+        // through a selected pointer and kept both in scratch memory)
+        float hv = 0.0f, adv = 0.0f;
         float bk[16];
         int bft = ft0;  // feature tile whose biases bk holds
         auto head_inputs = [&]() {
@@ -458,13 +467,11 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 bk[q] = tanh_bias(((gf32*)b2)[(int64_t)(32 * bft + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
             if (!kTrain || __builtin_amdgcn_readfirstlane(wave) >= kHW) return;
             const int64_t mc = valid ? m : p.rows - 1;  // clamped: unconditional loads, no branch
+            hv = (p.net == 0 ? p.logp_old : p.ret)[mc];
             if (p.net == 0) {
                 a0 = *reinterpret_cast<const float4*>(p.act + mc * kActPad + 4 * h);
                 a1 = *reinterpret_cast<const float4*>(p.act + mc * kActPad + 8 + 4 * h);
-                lo = p.logp_old[mc];
                 adv = p.adv[mc];
-            } else {
-                ret = p.ret[mc];
             }
         };
 #pragma unroll 1
@@ -557,6 +564,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                     for (int q = 4; q < 8; ++q) lp += h ? u[q] : t[q];      // o = 8..11
 #pragma unroll
                     for (int q = 4; q < 7; ++q) lp += h ? t[q] : u[q];      // o = 12..14
+                    const float lo = hv;
                     const float ratio = __expf(lp - lo);
                     const float A = (float)(((double)adv - adv_mean) / adv_div);
                     const float s1 = ratio * A;
@@ -588,7 +596,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 if (!kTrain) {
                     if (valid && h == 0) p.v_out[m] = v;
                 } else if (valid && h == 0) {
-                    const float e = v - ret;
+                    const float e = v - hv;  // hv: the return
                     d[0] = from_bf16(to_bf16(p.vf2 * e * p.sc));
                     db3[0] += d[0];
                     lsum[1] += e * e;

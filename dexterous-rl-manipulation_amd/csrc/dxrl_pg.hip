@@ -820,10 +820,11 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
 //   * env waves 0..3: lane (env 4w + row, s) exactly as k_pg_rollout_ls -- observation row,
 //     sampling, dynamics, contacts, termination, auto-reset;
 //   * aux waves 4..7: wave 4 + w is the lane-for-lane twin of env wave w.  While the env lanes
-//     step, the twin computes the NEXT step's Philox draws (action noise, dynamics noise,
-//     observation noise, the reset uniforms for both possible reset counters) and settles the
-//     PREVIOUS step's dense reward and episode bookkeeping (return, records, sums) from the
-//     inputs the env lanes left in LDS;
+//     step, the twin computes log pi and the act / log pi tape and settles the PREVIOUS step's
+//     dense reward and episode bookkeeping (return, records, sums) from the inputs the env lanes
+//     left in LDS;
+//   * in the head phase, one drawing wave per SIMD computes the step's Philox draws for all 16
+//     envs (step_draws);
 //   * all 8 waves split the actor MLP: one 32-column tile of L1 and of L2 each (two waves per
 //     SIMD, so one wave's tanh epilogue overlaps the other's MFMAs); aux wave 7 runs the mu head.
 // Every value is computed by the same instruction sequence as in k_pg_rollout_ls (same MFMA

@@ -428,6 +428,10 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             const int c = tid + kFThreads * u, row = c >> 3, col = 8 * (c & 7);
             *reinterpret_cast<bf16x8*>(X + row * kXp + col) = xr[u];
         }
+        // the first W1 fragments go out before the barrier (their L2 latency overlaps its wait;
+        // issued after the X stores, so they do not queue behind the X tile's HBM loads)
+        WPre<kIn / 16> pw1;
+        w_prefetch(pw1, W1, kIn / 16, ft0, lane);
         STAMP(0);
         __syncthreads();
         STAMP(1);
@@ -438,8 +442,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             // bias = W1 column 45 (X column 45 = 1)
-            WPre<kIn / 16> pw1;
-            w_prefetch(pw1, W1, kIn / 16, ft0 + j, lane);
+            if (j > 0) w_prefetch(pw1, W1, kIn / 16, ft0 + j, lane);
             EpiTanh e1{H1, 32 * (ft0 + j) + 4 * h, r, nullptr};
             fwd_pipe<kIn / 16, kXp, kMT>(pw1, X, lane, e1);
         }

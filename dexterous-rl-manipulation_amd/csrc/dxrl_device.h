@@ -64,9 +64,11 @@ __device__ __forceinline__ double u01_53(uint32_t hi, uint32_t lo) {
 }
 // 24-bit uniform in (0,1]
 __device__ __forceinline__ float u01_24(uint32_t v) { return ((float)(v >> 8) + 1.0f) * (1.0f / 16777216.0f); }
-// two standard normals (Box-Muller, f32) from two u32
+// two standard normals (Box-Muller, f32) from two u32.  Network-noise math, not parity math (no
+// CPU restatement replays these values: parity runs replay the device's action tape): hardware
+// log, sqrt and sin / cos, no correctly rounded sequences.
 __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& n0, float& n1) {
-    const float r = sqrtf(-2.0f * __logf(u01_24(a)));
+    const float r = __builtin_amdgcn_sqrtf(-2.0f * __logf(u01_24(a)));
     float s, c;
     __sincosf(6.28318530717958647692f * u01_24(b), &s, &c);
     n0 = r * c;

@@ -796,8 +796,89 @@ __global__ void k_slab_group_sum(const float* __restrict__ partial, int64_t slab
     tmp[(int64_t)g * slab + i] = s;
 }
 
+// float4 forms (slab, cols and ldo multiples of 4, 16-byte aligned bases): the same per-element
+// k order, four elements per thread (a quarter of the load instructions)
+__global__ void k_splitk_reduce4(const float4* __restrict__ partial, int64_t slab4, int z, float* __restrict__ out,
+                                 int accumulate, int cols, int64_t ldo) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= slab4) return;
+    float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int k = 0; k < z; ++k) {
+        const float4 v = partial[(int64_t)k * slab4 + i];
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+    }
+    const int64_t e = 4 * i;
+    const int64_t o = cols ? (e / cols) * ldo + e % cols : e;  // 4 | cols: the four stay in one row
+    float4* dst = reinterpret_cast<float4*>(out + o);
+    if (accumulate) {
+        const float4 a = *dst;
+        s = make_float4(a.x + s.x, a.y + s.y, a.z + s.z, a.w + s.w);
+    }
+    *dst = s;
+}
+
+// Both levels in one launch: a 256-thread block owns 16 float4 columns; thread (g, x) sums group g's
+// slabs of column x (in order), then the x column's 16 group sums are added in group order from
+// LDS -- exactly the two-launch sequence's per-element order, one launch and no tmp round trip.
+constexpr int kRX = 16;  // float4 columns per block (x 16 groups = 256 threads)
+__global__ __launch_bounds__(256) void k_slab_reduce2_4(const float4* __restrict__ partial, int64_t slab4, int z,
+                                                        float* __restrict__ out, int accumulate, int cols, int64_t ldo) {
+    __shared__ float4 grp[kReduceGroups][kRX];
+    const int x = threadIdx.x % kRX, g = threadIdx.x / kRX;
+    const int64_t i = (int64_t)blockIdx.x * kRX + x;
+    const int k0 = (int)((int64_t)g * z / kReduceGroups), k1 = (int)((int64_t)(g + 1) * z / kReduceGroups);
+    float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (i < slab4) {
+        for (int k = k0; k < k1; ++k) {
+            const float4 v = partial[(int64_t)k * slab4 + i];
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+    }
+    grp[g][x] = s;
+    __syncthreads();
+    if (g != 0 || i >= slab4) return;
+    float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int q = 0; q < kReduceGroups; ++q) {
+        const float4 v = grp[q][x];
+        r.x += v.x;
+        r.y += v.y;
+        r.z += v.z;
+        r.w += v.w;
+    }
+    const int64_t e = 4 * i;
+    const int64_t o = cols ? (e / cols) * ldo + e % cols : e;
+    float4* dst = reinterpret_cast<float4*>(out + o);
+    if (accumulate) {
+        const float4 a = *dst;
+        r = make_float4(a.x + r.x, a.y + r.y, a.z + r.z, a.w + r.w);
+    }
+    *dst = r;
+}
+
 int launch_slab_reduce(const float* partial, int64_t slab, int z, float* tmp, float* out, int accumulate,
                        hipStream_t st, int cols, int64_t ldo) {
+    const bool v4 = slab % 4 == 0 && cols % 4 == 0 && (cols == 0 || ldo % 4 == 0) &&
+                    (reinterpret_cast<uintptr_t>(partial) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+                    (!tmp || (reinterpret_cast<uintptr_t>(tmp) & 15) == 0);
+    if (v4) {
+        const int64_t slab4 = slab / 4;
+        const unsigned nb4 = (unsigned)((slab4 + 255) / 256);
+        if (z > kReduceGroups && tmp) {
+            hipLaunchKernelGGL(k_slab_reduce2_4, dim3((unsigned)((slab4 + kRX - 1) / kRX)), dim3(256), 0, st,
+                               reinterpret_cast<const float4*>(partial), slab4, z, out, accumulate, cols, ldo);
+            return launch_check("k_slab_reduce2_4");
+        }
+        hipLaunchKernelGGL(k_splitk_reduce4, dim3(nb4), dim3(256), 0, st, reinterpret_cast<const float4*>(partial), slab4,
+                           z, out, accumulate, cols, ldo);
+        return launch_check("k_splitk_reduce4");
+    }
     const unsigned nb = (unsigned)((slab + 255) / 256);
     if (z > kReduceGroups && tmp) {
         hipLaunchKernelGGL(k_slab_group_sum, dim3(nb, kReduceGroups), dim3(256), 0, st, partial, slab, z, tmp);

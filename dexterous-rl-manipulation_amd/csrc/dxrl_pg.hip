@@ -1471,9 +1471,18 @@ __global__ void k_gae_sums(const Moments* __restrict__ partial, int nb, double* 
     for (int k = threadIdx.x; k < nb; k += blockDim.x) a = merge(a, partial[k]);
     block_merge<256>(a, red);
     if (threadIdx.x == 0) {
-        stats[5] = red[0].n;
-        stats[6] = red[0].mean;
-        stats[7] = red[0].m2;
+        const Moments m = red[0];
+        stats[5] = m.n;
+        stats[6] = m.mean;
+        stats[7] = m.m2;
+        // the single-rank statistics as well (== dxrl_pg_adv_combine(stats + 5, world = 1), which
+        // a multi-rank caller runs afterwards over the all-gathered triples, overwriting these)
+        const Moments a1 = merge(Moments{0.0, 0.0, 0.0}, m);
+        stats[0] = a1.n;
+        stats[1] = a1.n * a1.mean;
+        stats[2] = a1.mean;
+        stats[3] = a1.m2;
+        stats[4] = sqrt(a1.m2 / (a1.n > 1.0 ? a1.n - 1.0 : 1.0));
     }
 }
 

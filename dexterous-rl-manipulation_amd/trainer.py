@@ -313,10 +313,9 @@ class PGTrainer:
         c = self.cfg
         N.call("dxrl_pg_gae", self.dev.index, N.ptr(self.rew), N.ptr(self.done), N.ptr(self.V[0]), self.n, self.T,
                c.gamma, c.lam, N.ptr(self.adv), N.ptr(self.ret), N.ptr(self.partial), N.ptr(self.stats), self._s())
-        # every rank's (count, mean, M2) in rank order, merged on device (identical on all ranks)
-        if self.world == 1:
-            N.call("dxrl_pg_adv_combine", self.dev.index, N.ptr(self.stats[5:]), 1, N.ptr(self.stats), self._s())
-        else:
+        # every rank's (count, mean, M2) in rank order, merged on device (identical on all ranks);
+        # one rank: dxrl_pg_gae already wrote the combined statistics
+        if self.world > 1:
             gather_adv_moments_(self.moments_all, self.stats, self.world, self.pg)
             N.call("dxrl_pg_adv_combine", self.dev.index, N.ptr(self.moments_all), self.world, N.ptr(self.stats),
                    self._s())

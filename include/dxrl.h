@@ -270,7 +270,8 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                     void* stream);
 
 /* GAE reverse scan; values f32 [(T+1) N]; writes adv/ret [T N] and this rank's advantage
- * moments stats[5] = T N, stats[6] = mean(adv), stats[7] = sum of squared deviations
+ * moments stats[5] = T N, stats[6] = mean(adv), stats[7] = sum of squared deviations, and
+ * stats[0..4] as dxrl_pg_adv_combine(stats + 5, world = 1) would (single rank: no second call)
  * (per-env sums about the env's own first value, merged with Chan et al.'s pairwise update
  * in a fixed order: no sum(a^2) - mean sum(a) cancellation).  partial: f64 [3 ceil(N / 64)];
  * stats: f64 [8]. */

@@ -774,15 +774,14 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     }
 }
 
-// grads blocks W1 / W3 (and log_std for the actor) from the workgroup sum (launch_slab_reduce)
-__global__ void k_fused_scatter(const float* __restrict__ sum, float* __restrict__ gW1, float* __restrict__ gW3,
-                                float* __restrict__ gLs, float* __restrict__ gW2, float ent_coef) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= kPartSize) return;
+// One element of the grads blocks W1 / W3 / log_std (actor) / W2's column 256 + pads from the
+// workgroup sum s = sum[j] (k_fused_scatter's mapping; `j` indexes the partial-slab layout)
+__device__ __forceinline__ void fused_scatter_one(int j, float s, float* __restrict__ gW1, float* __restrict__ gW3,
+                                                  float* __restrict__ gLs, float* __restrict__ gW2, float ent_coef) {
     if (j >= kPartB2) {  // W2 block column 256 (bias) and the zero pad columns 257..287 of row n
         const int n = j - kPartB2;
         if (n < kH) {
-            gW2[(int64_t)n * kHx + kH] = sum[kPartB2 + n];
+            gW2[(int64_t)n * kHx + kH] = s;
             for (int c = kH + 1; c < kHx; ++c) gW2[(int64_t)n * kHx + c] = 0.0f;
         }
         return;
@@ -790,13 +789,59 @@ __global__ void k_fused_scatter(const float* __restrict__ sum, float* __restrict
     const int col = (j - kPartW3) % kHx, orow = (j - kPartW3) / kHx;
     // never written by k_pg_fused: the pad columns 257.. and the dW3 rows 16..31 but their bias column
     const bool w3pad = j >= kPartW3 && j < kPartLs && (col > kH || (orow >= 16 && col < kH));
-    const float s = w3pad ? 0.0f : sum[j];
+    if (w3pad) s = 0.0f;
     if (j < kPartW3) gW1[j] = s;
     else if (j < kPartLs) gW3[j - kPartW3] = s;
     else if (gLs) {
         const int k = j - kPartLs;
         gLs[k] = k < kAct ? s - ent_coef : 0.0f;
     }
+}
+
+// The workgroup partials summed and scattered in one launch: a 256-thread block owns 16 float4
+// columns of the [z][kPartSize] slabs; with z > kReduceGroups thread (g, x) sums group g's slabs
+// of column x in order and the 16 group sums are added in group order (launch_slab_reduce's two
+// levels), else one thread sums the z slabs in order (its one level) -- the same per-element order
+// either way -- and the column goes straight into the grads blocks.
+__global__ __launch_bounds__(256) void k_fused_reduce_scatter(const float4* __restrict__ partial, int z,
+                                                              float* __restrict__ gW1, float* __restrict__ gW3,
+                                                              float* __restrict__ gLs, float* __restrict__ gW2,
+                                                              float ent_coef) {
+    constexpr int kRX = 16;
+    constexpr int64_t kSlab4 = kPartSize / 4;
+    static_assert(kPartSize % 4 == 0 && 256 == kRX * kReduceGroups, "layout");
+    __shared__ float4 grp[kReduceGroups][kRX];
+    const int x = threadIdx.x % kRX, g = threadIdx.x / kRX;
+    const int64_t i = (int64_t)blockIdx.x * kRX + x;
+    const auto add = [](float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); };
+    float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (z > kReduceGroups) {
+        const int k0 = (int)((int64_t)g * z / kReduceGroups), k1 = (int)((int64_t)(g + 1) * z / kReduceGroups);
+        float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (i < kSlab4)
+            for (int k = k0; k < k1; ++k) s = add(s, partial[(int64_t)k * kSlab4 + i]);
+        grp[g][x] = s;
+        __syncthreads();
+        if (g != 0 || i >= kSlab4) return;
+#pragma unroll
+        for (int q = 0; q < kReduceGroups; ++q) r = add(r, grp[q][x]);
+    } else {
+        if (g != 0 || i >= kSlab4) return;
+        for (int k = 0; k < z; ++k) r = add(r, partial[(int64_t)k * kSlab4 + i]);
+    }
+    const int j = (int)(4 * i);
+    fused_scatter_one(j, r.x, gW1, gW3, gLs, gW2, ent_coef);
+    fused_scatter_one(j + 1, r.y, gW1, gW3, gLs, gW2, ent_coef);
+    fused_scatter_one(j + 2, r.z, gW1, gW3, gLs, gW2, ent_coef);
+    fused_scatter_one(j + 3, r.w, gW1, gW3, gLs, gW2, ent_coef);
+}
+
+// grads blocks W1 / W3 (and log_std for the actor) from the workgroup sum (launch_slab_reduce)
+__global__ void k_fused_scatter(const float* __restrict__ sum, float* __restrict__ gW1, float* __restrict__ gW3,
+                                float* __restrict__ gLs, float* __restrict__ gW2, float ent_coef) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= kPartSize) return;
+    fused_scatter_one(j, sum[j], gW1, gW3, gLs, gW2, ent_coef);
 }
 
 }  // namespace
@@ -920,10 +965,20 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     // the pad columns 257..287 of the W3 slab are never written: the scatter zeroes them
     float* tmp = a->partial + (int64_t)grid * kPartSize;
     float* sum = tmp + (int64_t)kReduceGroups * kPartSize;
-    if (int rc = launch_slab_reduce(a->partial, kPartSize, grid, tmp, sum, 0, st)) return rc;
-    hipLaunchKernelGGL(k_fused_scatter, dim3((kPartSize + 255) / 256), dim3(256), 0, st, sum,
-                       G + (c ? kOffW1c : kOffW1a), G + o3, c ? nullptr : G + kOffLogStd, G + o2, (float)a->ent_coef);
-    if (int rc = launch_check("k_fused_scatter")) return rc;
+    if ((reinterpret_cast<uintptr_t>(a->partial) & 15) == 0) {
+        (void)tmp;
+        (void)sum;
+        hipLaunchKernelGGL(k_fused_reduce_scatter, dim3((unsigned)((kPartSize / 4 + 15) / 16)), dim3(256), 0, st,
+                           reinterpret_cast<const float4*>(a->partial), grid, G + (c ? kOffW1c : kOffW1a), G + o3,
+                           c ? nullptr : G + kOffLogStd, G + o2, (float)a->ent_coef);
+        if (int rc = launch_check("k_fused_reduce_scatter")) return rc;
+    } else {
+        if (int rc = launch_slab_reduce(a->partial, kPartSize, grid, tmp, sum, 0, st)) return rc;
+        hipLaunchKernelGGL(k_fused_scatter, dim3((kPartSize + 255) / 256), dim3(256), 0, st, sum,
+                           G + (c ? kOffW1c : kOffW1a), G + o3, c ? nullptr : G + kOffLogStd, G + o2,
+                           (float)a->ent_coef);
+        if (int rc = launch_check("k_fused_scatter")) return rc;
+    }
     // dW2[:, 0..255] = dH2^T H1 (the bias column 256 came from the column sums above)
     if (recompute)
         return launch_wgrad_l1(static_cast<const bf16*>(a->dh2), kH, f.X, kIn, w + (c ? kBfW1c : kBfW1a), a->rows,

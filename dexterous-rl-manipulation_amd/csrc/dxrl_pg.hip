@@ -1024,16 +1024,17 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         box_muller(r.x, r.y, nz[0], nz[1]);
         box_muller(r.z, r.w, nz[2], nz[3]);
     };
-    // Step t's action / dynamics noise and reset uniforms, computed in the head phase by waves
-    // that each have a SIMD to themselves for it (waves w and w + 4 share SIMD w; Philox's 64-bit
-    // products are quarter-rate, so two drawing waves on one SIMD serialise): one Philox block per
-    // lane, keys (KEYS) and reset counters (RW[.].rctr) of all 16 envs from LDS, values written
-    // straight into the consumers' slots.
-    //   wave 0 (SIMD 0)        action noise: lane -> (env lane >> 2, block lane & 3)
-    //   waves 1, 2, 7 (SIMD 1, 2, 3 -- 3 runs the head on the matrix core): group lane g < 176
-    //                          reset block g % 11 of env g / 11 (u01_53 of both halves: joint
-    //                          slots 0..14 -> u1, extra slots 15..20 -> u2)
-    //   wave 4 (SIMD 0)        dynamics noise (robustness configs only), as wave 0
+    // Step t's action / dynamics noise and reset uniforms, computed in the head phase by the aux
+    // waves, one per SIMD (waves w and w + 4 share SIMD w; Philox's 64-bit products are
+    // quarter-rate, so two drawing waves on one SIMD serialise), while the env waves run the
+    // action-independent object update (env_object_step) and wave 3 the mu head: one Philox block
+    // per lane, keys (KEYS) and reset counters (RW[.].rctr) of all 16 envs from LDS, values
+    // written straight into the consumers' slots.
+    //   wave 4 (SIMD 0)        action noise: lane -> (env lane >> 2, block lane & 3); then the
+    //                          dynamics noise in robustness configs
+    //   waves 5, 6, 7 (SIMD 1, 2, 3 -- 3 also runs the head on the matrix core): group lane
+    //                          g < 176 reset block g % 11 of env g / 11 (u01_53 of both halves:
+    //                          joint slots 0..14 -> u1, extra slots 15..20 -> u2)
     constexpr int kResetBlocks = (kReset + 1) / 2;
     const auto step_draws = [&](uint64_t ctr, int64_t t_) {
         // the lane id re-read each step (volatile): the task indices and LDS addresses derived
@@ -1041,23 +1042,26 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         // pressure into spills (each reload a vmcnt(0))
         int lane;
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-        if (wave == 0 || (wave == 4 && dyn_noise)) {
+        if (wave == 4) {
             const int e = lane >> 2, blk = lane & 3;
             if ((int64_t)blockIdx.x * kLsEnvs + e >= n) return;
-            const uint32_t stream = wave == 0 ? kStreamPolicy : kStreamDyn;
-            const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)blk},
-                                   KEYS[e][2], KEYS[e][3]);
-            float nz[4];
-            box_muller(r.x, r.y, nz[0], nz[1]);
-            box_muller(r.z, r.w, nz[2], nz[3]);
-            float* dst = wave == 0 ? DR.eps : DR.dzn;
+#pragma unroll 1
+            for (int pass = 0; pass < (dyn_noise ? 2 : 1); ++pass) {
+                const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), pass ? kStreamDyn : kStreamPolicy,
+                                             (uint32_t)blk},
+                                       KEYS[e][2], KEYS[e][3]);
+                float nz[4];
+                box_muller(r.x, r.y, nz[0], nz[1]);
+                box_muller(r.z, r.w, nz[2], nz[3]);
+                float* dst = pass ? DR.dzn : DR.eps;
 #pragma unroll
-            for (int h = 0; h < 4; ++h)
-                if (4 * blk + h < kAct) dst[16 * e + 4 * blk + h] = nz[h];
+                for (int h = 0; h < 4; ++h)
+                    if (4 * blk + h < kAct) dst[16 * e + 4 * blk + h] = nz[h];
+            }
             return;
         }
-        if (wave != 1 && wave != 2 && wave != 7) return;
-        const int g = 64 * (wave == 7 ? 2 : wave - 1) + lane;
+        if (wave < 5) return;
+        const int g = 64 * (wave - 5) + lane;
         if (g >= kLsEnvs * kResetBlocks) return;
         const int e = g / kResetBlocks, blk = g % kResetBlocks;
         if ((int64_t)blockIdx.x * kLsEnvs + e >= n) return;
@@ -1147,6 +1151,27 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     };
     const bool mlp = !(p.diag & 1), env_on = !(p.diag & 2);
     // ---- env lanes, P4 of step t: action, dynamics, contacts, termination, auto-reset
+    // ---- env lanes, head phase of step t: the object's velocity damping, gravity, position and
+    // wall stops (ME:212-235) -- independent of the action, so off the P4 chain (the env waves
+    // wait for the head and the draws here anyway)
+    const auto env_object_step = [&]() {
+        const double damp = 1.0 - (fric * 0.1 * 0.01);
+        const float dampf = (float)damp;
+        const bool op32 = (flags & kOpIsF32) != 0, fric_f64 = (flags & kFricF64) != 0;
+        const int ax = s < 3 ? s : 0;
+        const double gz = ax == 2 ? kGz : 0.0, lo = ax == 2 ? 0.0 : -0.2, hi = ax == 2 ? 0.3 : 0.2;
+        float v = fric_f64 ? (float)((double)ovd * damp) : ovd * dampf;
+        v = (float)((double)v + gz);
+        const float inc = v * kDt;
+        double q = op32 ? (double)((float)opd + inc) : opd + (double)inc;
+        q = clipd(q, lo, hi);
+        if ((q <= lo && v < 0.0f) || (q >= hi && v > 0.0f)) v = 0.0f;
+        if (s < 3) {
+            opd = q;
+            ovd = v;
+        }
+        flags &= ~kOpIsF32;
+    };
     const auto env_lane_step = [&](int64_t t, int64_t m) {
         const float mu = mlp ? MU[eg * (kOut + 1) + sa] : 0.0f;
         float a = mu + SIG[sa] * DR.eps[et_tid];
@@ -1160,24 +1185,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
                 jv = kC09 * jv + kC01 * ak;
                 jp = clipf(jp + jv * kDt, -1.0f, 1.0f);
             }
-            {
-                const double damp = 1.0 - (fric * 0.1 * 0.01);
-                const float dampf = (float)damp;
-                const bool op32 = (flags & kOpIsF32) != 0, fric_f64 = (flags & kFricF64) != 0;
-                const int ax = s < 3 ? s : 0;
-                const double gz = ax == 2 ? kGz : 0.0, lo = ax == 2 ? 0.0 : -0.2, hi = ax == 2 ? 0.3 : 0.2;
-                float v = fric_f64 ? (float)((double)ovd * damp) : ovd * dampf;
-                v = (float)((double)v + gz);
-                const float inc = v * kDt;
-                double q = op32 ? (double)((float)opd + inc) : opd + (double)inc;
-                q = clipd(q, lo, hi);
-                if ((q <= lo && v < 0.0f) || (q >= hi && v > 0.0f)) v = 0.0f;
-                if (s < 3) {
-                    opd = q;
-                    ovd = v;
-                }
-            }
-            flags &= ~kOpIsF32;
+            // (the object's update, which does not depend on the action, ran in the head phase:
+            // env_object_step)
             double op3[3];
             row_object(opd, op3);
             double dmin;
@@ -1291,6 +1300,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
                                                                     &b2_reg);
         WS_STAMP(2);
         lds_barrier();
+        if (!aux && live && env_on) env_object_step();
         if (mlp && wave == kHeadWave) {  // mu head: 16 env rows x 32 head rows
             f32x16 acc;
 #pragma unroll
@@ -1320,7 +1330,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         if (!(p.diag & 256)) {
             // this step's draws (RW[(t - 1) & 1].rctr: the counters after step t-1's resets), the next
             // observation row's noise (aux lanes, own rows)
-            if (wave != kHeadWave) step_draws(ctr, t);
+            if (aux) step_draws(ctr, t);
             if (aux && live) obs_draws(ctr + 1);
         }
         WS_STAMP(3);

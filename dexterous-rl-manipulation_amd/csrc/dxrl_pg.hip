@@ -823,8 +823,8 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
 //     step, the twin computes log pi and the act / log pi tape and settles the PREVIOUS step's
 //     dense reward and episode bookkeeping (return, records, sums) from the inputs the env lanes
 //     left in LDS;
-//   * in the head phase, one drawing wave per SIMD computes the step's Philox draws for all 16
-//     envs (step_draws);
+//   * in the head phase, one drawing aux wave per SIMD computes the step's Philox draws for all
+//     16 envs (step_draws) while the env waves run the action-independent object update;
 //   * all 8 waves split the actor MLP: one 32-column tile of L1 and of L2 each (two waves per
 //     SIMD, so one wave's tanh epilogue overlaps the other's MFMAs); aux wave 7 runs the mu head.
 // Every value is computed by the same instruction sequence as in k_pg_rollout_ls (same MFMA
@@ -869,9 +869,10 @@ struct WsReward {      // an env's dense-reward inputs and episode end of one st
 //   P0  env lanes write the observation row (+ observation noise drawn in step t-1's P3)
 //   P1  all waves: L1, one 32-column tile each            (the env lanes also store the obs row)
 //   P2  all waves: L2, one 32-column tile each
-//   P3  env wave 3: the mu head.  In its shadow, one drawing wave per SIMD (step_draws): wave 0
-//       step t's action noise, waves 1, 2, 7 the reset uniforms at each env's exact counter (step
-//       t-1's episode end is known); aux lanes: step t+1's observation noise
+//   P3  env wave 3: the mu head; all env waves: the object update (env_object_step).  In their
+//       shadow, one drawing aux wave per SIMD (step_draws): wave 4 step t's action noise, waves
+//       5, 6, 7 the reset uniforms at each env's exact counter (step t-1's episode end is known);
+//       aux lanes: step t+1's observation noise
 //   P4  env lanes: a = mu + sigma eps, dynamics, contacts, termination, auto-reset.
 //       Aux lanes: the same a, log pi (DPP row sum in action order), the act / log pi tape, then
 //       settle step t-1's reward and episode bookkeeping

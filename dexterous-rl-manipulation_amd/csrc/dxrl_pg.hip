@@ -228,6 +228,43 @@ __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfr
     }
 }
 
+// 16-row tiles on v_mfma_f32_16x16x32_bf16 for a 16-env workgroup: one wave computes the 16
+// activation rows x 16*NT columns with no dead MFMA rows (wave_layer's RT == 1 tile carries 16
+// live rows in a 32-row MFMA: twice the matrix-core cycles per output).  A chain of 16x16x32
+// MFMAs over k-steps of 32 rounds exactly as the 32x32x16 chain over the same k order
+// (tools/mfma_order.hip: 0 of 131,072 outputs differ), so the hidden units stay bit-identical to
+// the learner's forward and to k_pg_rollout_ls.  Lane l: A row l & 15, k 32 k + 8 (l >> 4) ..+7;
+// wfrag(j, k) = W[n0 + 16 j + (l & 15)][32 k + 8 (l >> 4) ..+7]; accumulator: column l & 15,
+// rows 4 (l >> 4) .. +3.  Activation fragments stream through a ring kD k-steps ahead (pinned
+// by scheduling barriers); bias_v[j]: the bias of column n0 + 16 j + (l & 15) (or null: none).
+template <int KS, int NT, typename WF>
+__device__ __forceinline__ void wave_layer16(const bf16* A, int lda, const WF& wfrag, int n0, bf16* out, int ldo,
+                                             int lane, const float* bias_v = nullptr) {
+    const int r = lane & 15, g = lane >> 4;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    constexpr int kD = KS < 4 ? KS : 4;
+    bf16x8 a[kD];
+#pragma unroll
+    for (int k = 0; k < kD; ++k) a[k] = *reinterpret_cast<const bf16x8*>(A + r * lda + 32 * k + 8 * g);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[j] = mfma16(a[k % kD], wfrag(j, k), acc[j]);
+        if (k + kD < KS) a[k % kD] = *reinterpret_cast<const bf16x8*>(A + r * lda + 32 * (k + kD) + 8 * g);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int n = n0 + 16 * j + r;
+        const float bk = tanh_bias(bias_v ? bias_v[j] : 0.0f);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(4 * g + q) * ldo + n] = to_bf16(tanh_pre(acc[j][q], bk));
+    }
+}
+
 // 4 waves (one per SIMD, so a wave may use 256 VGPRs + 256 AGPRs): wave w owns hidden
 // columns kCpw*w .. kCpw*w + kCpw - 1 of both hidden layers; waves 2, 3 compute the mu head.
 constexpr int kRolloutWaves = 4, kCpw = kH / kRolloutWaves, kNT = kCpw / 32;
@@ -905,8 +942,14 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         SIG[tid] = __expf(ls);
         ISIG[tid] = __expf(-ls);
     }
-    WTile<kH / 16> w2;  // this wave's L2 column tile
-    load_wtile(w2, p.wbf + kBfW2a, kHx, 32 * wave, lane);
+    // this wave's L2 columns 32 wave .. + 31 as two 16-column tiles of 16x16x32 fragments
+    bf16x8 w2[2][kH / 32];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int k = 0; k < kH / 32; ++k)
+            w2[j][k] = *reinterpret_cast<const bf16x8*>(p.wbf + kBfW2a + (int64_t)(32 * wave + 16 * j + (lane & 15)) * kHx +
+                                                        32 * k + 8 * (lane >> 4));
     for (int c = tid; c < kH * (kIn / 8); c += kWsThreads) {
         const int row = c / (kIn / 8), col = 8 * (c % (kIn / 8));
         *reinterpret_cast<bf16x8*>(W1s + row * kW1s + col) =
@@ -925,14 +968,16 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         H1[kLsEnvs * kHs + c] = (bf16)0.0f;
         H2[kLsEnvs * kHs + c] = (bf16)0.0f;
     }
-    const int r32 = lane & 31, h2 = lane >> 5;
-    const auto w1frag = [&](int, int k) {
-        return *reinterpret_cast<const bf16x8*>(W1s + (32 * wave + r32) * kW1s + 16 * k + 8 * h2);
+    const int r16 = lane & 15, g16 = lane >> 4;  // 16x16x32 fragment row / k group
+    const auto w1frag = [&](int j, int k) {
+        return *reinterpret_cast<const bf16x8*>(W1s + (32 * wave + 16 * j + r16) * kW1s + 32 * k + 8 * g16);
     };
-    const auto w2frag = [&](int, int k) { return w2.b[k]; };
-    // step-invariant biases in registers: L2 column 32 wave + r32, head row r32
-    const float b2_reg = p.params[kOffW2a + (int64_t)(32 * wave + r32) * kHx + kH];
-    const float b3_reg = p.params[kOffW3a + (int64_t)r32 * kHx + kH];
+    const auto w2frag = [&](int j, int k) { return w2[j][k]; };
+    // step-invariant biases in registers: L2 columns 32 wave + 16 j + r16, head row r16
+    float b2_reg[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b2_reg[j] = p.params[kOffW2a + (int64_t)(32 * wave + 16 * j + r16) * kHx + kH];
+    const float b3_reg = p.params[kOffW3a + (int64_t)r16 * kHx + kH];
 
     // ---- env-lane state (env waves) / episode bookkeeping (aux waves)
     float jp = 0.0f, jv = 0.0f;
@@ -1293,40 +1338,36 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         WS_STAMP(0);
         lds_barrier();
         if (!aux && live) tape_obs_row(m);
-        if (mlp) wave_layer<kIn / 16, 1, true, 1>(X, kXs, w1frag, 32 * wave, nullptr, 0, H1, kHs, lane);
+        if (mlp) wave_layer16<kIn / 32, 2>(X, kXs, w1frag, 32 * wave, H1, kHs, lane);  // b: col 45
         WS_STAMP(1);
         lds_barrier();
-        if (mlp)
-            wave_layer<kH / 16, 1, true, 1, decltype(w2frag), true>(H1, kHs, w2frag, 32 * wave, nullptr, 0, H2, kHs, lane,
-                                                                    &b2_reg);
+        if (mlp) wave_layer16<kH / 32, 2>(H1, kHs, w2frag, 32 * wave, H2, kHs, lane, b2_reg);
         WS_STAMP(2);
         lds_barrier();
         if (!aux && live && env_on) env_object_step();
-        if (mlp && wave == kHeadWave) {  // mu head: 16 env rows x 32 head rows
-            f32x16 acc;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-            // H2 rows and W3 rows (head outputs) from LDS: a ring of 4 k-steps of fragments,
-            // refilled 4 ahead (pinned by scheduling barriers, as in wave_layer)
+        if (mlp && wave == kHeadWave) {  // mu head: 16 env rows x head rows 0..15 (15 live)
+            f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+            // H2 rows and W3 rows (head outputs) from LDS as 16x16x32 fragments: a ring of 4
+            // k-steps, refilled 4 ahead (pinned by scheduling barriers, as in wave_layer16)
             constexpr int kD = 4;
             bf16x8 ah[kD], bw[kD];
 #pragma unroll
             for (int k = 0; k < kD; ++k) {
-                ah[k] = *reinterpret_cast<const bf16x8*>(H2 + r32 * kHs + 16 * k + 8 * h2);
-                bw[k] = *reinterpret_cast<const bf16x8*>(W3s + r32 * kW3s + 16 * k + 8 * h2);
+                ah[k] = *reinterpret_cast<const bf16x8*>(H2 + r16 * kHs + 32 * k + 8 * g16);
+                bw[k] = *reinterpret_cast<const bf16x8*>(W3s + r16 * kW3s + 32 * k + 8 * g16);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int k = 0; k < kH / 16; ++k) {
-                acc = mfma32(ah[k % kD], bw[k % kD], acc);
-                if (k + kD < kH / 16) {
-                    ah[k % kD] = *reinterpret_cast<const bf16x8*>(H2 + r32 * kHs + 16 * (k + kD) + 8 * h2);
-                    bw[k % kD] = *reinterpret_cast<const bf16x8*>(W3s + r32 * kW3s + 16 * (k + kD) + 8 * h2);
+            for (int k = 0; k < kH / 32; ++k) {
+                acc = mfma16(ah[k % kD], bw[k % kD], acc);
+                if (k + kD < kH / 32) {
+                    ah[k % kD] = *reinterpret_cast<const bf16x8*>(H2 + r16 * kHs + 32 * (k + kD) + 8 * g16);
+                    bw[k % kD] = *reinterpret_cast<const bf16x8*>(W3s + r16 * kW3s + 32 * (k + kD) + 8 * g16);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
-            for (int q = 0; q < 8; ++q) MU[acc_row(q, lane) * (kOut + 1) + r32] = acc[q] + b3_reg;  // rows < 16
+            for (int q = 0; q < 4; ++q) MU[(4 * g16 + q) * (kOut + 1) + r16] = acc[q] + b3_reg;
         }
         if (!(p.diag & 256)) {
             // this step's draws (RW[(t - 1) & 1].rctr: the counters after step t-1's resets), the next

@@ -231,12 +231,15 @@ __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfr
 // 16-row tiles on v_mfma_f32_16x16x32_bf16 for a 16-env workgroup: one wave computes the 16
 // activation rows x 16*NT columns with no dead MFMA rows (wave_layer's RT == 1 tile carries 16
 // live rows in a 32-row MFMA: twice the matrix-core cycles per output).  A chain of 16x16x32
-// MFMAs over k-steps of 32 rounds exactly as the 32x32x16 chain over the same k order
+// MFMAs over k-steps of 32 rounds exactly like the 32x32x16 chain over the same k order
 // (tools/mfma_order.hip: 0 of 131,072 outputs differ), so the hidden units stay bit-identical to
-// the learner's forward and to k_pg_rollout_ls.  Lane l: A row l & 15, k 32 k + 8 (l >> 4) ..+7;
-// wfrag(j, k) = W[n0 + 16 j + (l & 15)][32 k + 8 (l >> 4) ..+7]; accumulator: column l & 15,
-// rows 4 (l >> 4) .. +3.  Activation fragments stream through a ring kD k-steps ahead (pinned
-// by scheduling barriers); bias_v[j]: the bias of column n0 + 16 j + (l & 15) (or null: none).
+// the learner's forward and to k_pg_rollout_ls.  Transposed formulation (weights as the A
+// operand, as in the learner): lane l's accumulator holds columns n0 + 16 j + 4 (l >> 4) .. +3 of
+// activation row l & 15, so the tanh epilogue runs on packed pairs and leaves as one 8-byte LDS
+// store per tile.  Fragments: A row l & 15, k 32 k + 8 (l >> 4) ..+7; wfrag(j, k) =
+// W[n0 + 16 j + (l & 15)][32 k + 8 (l >> 4) ..+7].  Activation fragments stream through a ring
+// kD k-steps ahead (pinned by scheduling barriers).  bias_v[4 j + q]: the bias of column
+// n0 + 16 j + 4 (l >> 4) + q (or null: none).
 template <int KS, int NT, typename WF>
 __device__ __forceinline__ void wave_layer16(const bf16* A, int lda, const WF& wfrag, int n0, bf16* out, int ldo,
                                              int lane, const float* bias_v = nullptr) {
@@ -252,16 +255,22 @@ __device__ __forceinline__ void wave_layer16(const bf16* A, int lda, const WF& w
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[j] = mfma16(a[k % kD], wfrag(j, k), acc[j]);
+        for (int j = 0; j < NT; ++j) acc[j] = mfma16(wfrag(j, k), a[k % kD], acc[j]);
         if (k + kD < KS) a[k % kD] = *reinterpret_cast<const bf16x8*>(A + r * lda + 32 * (k + kD) + 8 * g);
         __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-        const int n = n0 + 16 * j + r;
-        const float bk = tanh_bias(bias_v ? bias_v[j] : 0.0f);
+        bf16x4 v;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) out[(4 * g + q) * ldo + n] = to_bf16(tanh_pre(acc[j][q], bk));
+        for (int q = 0; q < 4; q += 2) {
+            const f32x2 b = bias_v ? f32x2{tanh_bias(bias_v[4 * j + q]), tanh_bias(bias_v[4 * j + q + 1])}
+                                   : f32x2{0.0f, 0.0f};
+            const f32x2 t = tanh_pre2(f32x2{acc[j][q], acc[j][q + 1]}, b);
+            v[q] = to_bf16(t.x);
+            v[q + 1] = to_bf16(t.y);
+        }
+        *reinterpret_cast<bf16x4*>(out + r * ldo + n0 + 16 * j + 4 * g) = v;
     }
 }
 
@@ -973,10 +982,13 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         return *reinterpret_cast<const bf16x8*>(W1s + (32 * wave + 16 * j + r16) * kW1s + 32 * k + 8 * g16);
     };
     const auto w2frag = [&](int j, int k) { return w2[j][k]; };
-    // step-invariant biases in registers: L2 columns 32 wave + 16 j + r16, head row r16
-    float b2_reg[2];
+    // step-invariant biases in registers: L2 columns 32 wave + 16 j + 4 g16 + q, head row r16
+    float b2_reg[8];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) b2_reg[j] = p.params[kOffW2a + (int64_t)(32 * wave + 16 * j + r16) * kHx + kH];
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            b2_reg[4 * j + q] = p.params[kOffW2a + (int64_t)(32 * wave + 16 * j + 4 * g16 + q) * kHx + kH];
     const float b3_reg = p.params[kOffW3a + (int64_t)r16 * kHx + kH];
 
     // ---- env-lane state (env waves) / episode bookkeeping (aux waves)

@@ -494,6 +494,19 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             fwd_run<kH / 16, kHp, kMT>(pw2, H1, acc, lane, l2_hook, (p.diag & 32) != 0);
             if (!(p.diag & 16)) store_hidden(acc, ft0 + j, bk, H2, lane);
         }
+        // forward mode: the head waves' W3 fragments, all 16 k-steps, go out before the barrier
+        // (their L2 latency overlaps its wait instead of opening the head phase twice).  Train
+        // mode keeps two batches of 8 issued in the head: 16 in flight there spill (the
+        // launch-long gradient accumulators are live)
+        constexpr int kW3K = kH / 16;
+        bf16x8 w3p[kTrain ? 1 : kW3K];
+        const gbf16x8* w3row = (const gbf16x8*)W3 + lane;  // fragment stream, feature tile 0
+        if constexpr (!kTrain) {
+            if (wave < kHW) {
+#pragma unroll
+                for (int k = 0; k < kW3K; ++k) w3p[k] = w3row[64 * k];
+            }
+        }
         STAMP(4);
         __syncthreads();
         STAMP(5);
@@ -508,26 +521,32 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         if (wave < kHW) {
             f32x16 acc;
             zero_acc(acc);
-            // W3 fragments in two batches of 8 (32 registers in flight)
-            const gbf16x8* wrow = (const gbf16x8*)W3 + lane;  // fragment stream, feature tile 0
-            constexpr int kB = kH / 32;  // fragments per batch (two batches: 32 registers in flight)
-            bf16x8 w3f[kB];
+            if constexpr (!kTrain) {
 #pragma unroll
-            for (int k = 0; k < kB; ++k) w3f[k] = wrow[64 * k];
-            __builtin_amdgcn_sched_barrier(0);
+                for (int k = 0; k < kW3K; ++k) {
+                    const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * k + 8 * h);
+                    acc = mfma32(w3p[k], b, acc);
+                }
+            } else {
+                constexpr int kB = kW3K / 2;  // fragments per batch (32 registers in flight)
+                bf16x8 w3f[kB];
 #pragma unroll
-            for (int k = 0; k < kB; ++k) {
-                const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * k + 8 * h);
-                acc = mfma32(w3f[k], b, acc);
-            }
-            __builtin_amdgcn_sched_barrier(0);
+                for (int k = 0; k < kB; ++k) w3f[k] = w3row[64 * k];
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int k = 0; k < kB; ++k) w3f[k] = wrow[64 * (k + kB)];
-            __builtin_amdgcn_sched_barrier(0);
+                for (int k = 0; k < kB; ++k) {
+                    const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * k + 8 * h);
+                    acc = mfma32(w3f[k], b, acc);
+                }
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int k = 0; k < kB; ++k) {
-                const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * (k + kB) + 8 * h);
-                acc = mfma32(w3f[k], b, acc);
+                for (int k = 0; k < kB; ++k) w3f[k] = w3row[64 * (k + kB)];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 0; k < kB; ++k) {
+                    const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * (k + kB) + 8 * h);
+                    acc = mfma32(w3f[k], b, acc);
+                }
             }
             float d[8], b3v[8];
 #pragma unroll

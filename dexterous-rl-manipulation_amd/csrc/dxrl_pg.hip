@@ -1185,24 +1185,23 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             ep_ret = 0.0;
         }
     };
+    // lane s's elements row_obs_elem(s, 0..3): joint position, joint velocity, object position /
+    // identity quaternion (ME:164) / finger contact, object velocity -- the values selected
+    // without divergent branches, then at most four predicated 2-byte stores (the if / else-if
+    // chain compiled to a serial walk of exec-masked regions on the env waves' critical path)
     const auto write_obs_row = [&]() {
         bf16* xr = X + eg * kXs;
-        const auto put = [&](int j, float v) {
+        const auto put = [&](int j, float v, int k) {
             if (obs_noise) v = v + p.obs_noise * DR.on[j][et_tid];
-            xr[row_obs_elem(s, j)] = to_bf16(v);
+            xr[k] = to_bf16(v);
         };
+        const float v2 = s < 3 ? (float)opd : (s < 7 ? (s == 3 ? 1.0f : 0.0f) : (float)((flags >> ((s - 7) & 31)) & 1u));
         if (s < kD) {
-            put(0, jp);
-            put(1, jv);
+            put(0, jp, s);
+            put(1, jv, kD + s);
         }
-        if (s < 3) {
-            put(2, (float)opd);
-            put(3, ovd);
-        } else if (s < 7) {
-            put(2, s == 3 ? 1.0f : 0.0f);  // identity quaternion (ME:164)
-        } else if (s < 7 + kF) {
-            put(2, (float)((flags >> (s - 7)) & 1u));
-        }
+        if (s < 7 + kF) put(2, v2, s < 7 ? 2 * kD + s : 2 * kD + 3 + s);
+        if (s < 3) put(3, ovd, 2 * kD + 7 + s);
     };
     const auto tape_obs_row = [&](int64_t m) {
         *reinterpret_cast<bf16x4*>(p.obs_rm + m * kIn + 4 * s) = *reinterpret_cast<const bf16x4*>(X + eg * kXs + 4 * s);

@@ -75,6 +75,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--dist", action="store_true",
+                   help="create the RCCL process group even at --gpus 1 (before any GPU work) and run the "
+                        "multi-rank code path: the trainer's collectives, barrier and max-over-ranks timing")
     a = p.parse_args()
     w = WORKLOADS[a.config]
     a.envs = a.envs or w["envs"]
@@ -104,28 +107,42 @@ def launch_ranks(args) -> int:
 
 
 def dist_setup(args):
+    """One rank per GPU over RCCL (torch.distributed "nccl").  With --dist a world-1 process
+    group is created too, so the collectives run exactly as in a multi-rank job."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
-    if world > 1:
+    if world > 1 or args.dist:
+        import socket
         import torch.distributed as dist
+        if "MASTER_PORT" not in os.environ:  # plain `bench.py --dist` (no torchrun)
+            s = socket.socket()
+            s.bind(("127.0.0.1", 0))
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+            s.close()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
     else:
         torch.cuda.set_device(0)
     return world, rank, local
 
 
+def _dist_on():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def barrier(world):
-    if world > 1:
+    if _dist_on():
         import torch.distributed as dist
         dist.barrier()
 
 
 def max_over_ranks(x, world, dev):
-    if world == 1:
+    if not _dist_on():
         return x
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64, device=dev)
@@ -145,7 +162,7 @@ def pg_bench(args, world, rank, dev):
     MLP fused) + critic forward + GAE + adv-norm + actor forward + heads + backward +
     RCCL gradient all-reduce (world > 1) + Adam."""
     pg = None
-    if world > 1:
+    if _dist_on():  # world > 1, or --dist: the trainer runs its collectives over RCCL
         import torch.distributed as dist
         pg = dist.group.WORLD
     env, tr = build_pg_workload(args.config, dev, rank=rank, world=world, process_group=pg, envs=args.envs,
@@ -263,17 +280,22 @@ def step_kernel_roofline(args, dev):
     """k_step at large N: algorithmic bytes / HIP-event time per launch."""
     n = args.roofline_envs
     ms = step_kernel_time(n, args.roofline_launches, dev)
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
-    if os.path.exists(pmc):
+    # traffic: PMC-corrected HBM bytes per launch (2 FETCH_SIZE + WRITE_SIZE, separate --pmc passes,
+    # tools/profile_round.sh) from the newest round's profiles/rNN/pmc_step_kernel.json
+    traffic, src = None, None
+    import glob
+    for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "pmc_step_kernel.json")), reverse=True):
         with open(pmc) as f:
             d = json.load(f)
         if d.get("envs") == n:
-            traffic = d.get("hbm_bytes_per_launch")
+            traffic, src = d.get("hbm_bytes_per_launch"), os.path.relpath(pmc, ROOT)
+            break
     bytes_per_launch = STEP_BYTES_PER_ENV * n
     achieved = bytes_per_launch / (ms * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "kernel": "k_step (dxrl_env_step)",
+            "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": src,
+            "traffic_per_algorithmic_byte": round(traffic / bytes_per_launch, 4) if traffic else None,
+            "kernel": "k_step (dxrl_env_step)",
             "envs": n, "bytes_per_env_step": STEP_BYTES_PER_ENV, "ms_per_launch": round(ms, 4),
             "env_steps_per_s": round(n / (ms * 1e-3), 1)}
 
@@ -369,8 +391,8 @@ def main():
                     f"{args.horizon} env steps x {args.envs} envs + critic fwd + GAE + adv-norm + PPO-clip / value "
                     f"heads + backward + Adam ({upd})")
         dtype = "bf16 MFMA (f32 acc) + f32/f64 env"
-        par = (f"dp{world} (env shards; RCCL all-reduce of the f64 advantage moments and the f32 grads)"
-               if world > 1 else "dp1")
+        par = (f"dp{world} (env shards; RCCL all-gather of the f64 advantage moments, all-reduce of the f32 "
+               f"grads)" if world > 1 or args.dist else "dp1")
         extra = {"phases_ms": phases, "mfma": mfma, "train_stats": stats}
     else:
         wall, kernel_ms = rollout_bench(args, world, rank, dev)
@@ -388,7 +410,8 @@ def main():
         "data": "synthetic (device Philox4x32-10 reset draws, policy / learner noise; random-init weights)",
         "config": {"workload": workload, "learner": args.learner, "envs_per_gpu": args.envs,
                    "global_envs": args.envs * world, "horizon": args.horizon, "parallelism": par,
-                   "world_size": world, "backend": "nccl (RCCL over xGMI)" if world > 1 else None},
+                   "world_size": world,
+                   "backend": "nccl (RCCL over xGMI)" if world > 1 or args.dist else None},
     }
     out.update(extra)
     if rank == 0 and not args.no_roofline:
@@ -398,7 +421,7 @@ def main():
         out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out))
-    if world > 1:
+    if _dist_on():
         import torch.distributed as dist
         dist.destroy_process_group()
 

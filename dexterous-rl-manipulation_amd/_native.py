@@ -80,7 +80,8 @@ class PgRolloutArgs(C.Structure):
                                           "ep_sum_return", "ep_sum_length", "ep_successes")] + \
                [("diag_flags", C.c_int32), ("success_rule", C.c_int32), ("record_cap", C.c_int32),
                 ("rec_return", C.c_void_p), ("rec_length", C.c_void_p), ("rec_success", C.c_void_p),
-                ("rec_end_step", C.c_void_p), ("ep_code", C.c_void_p), ("applied_act", C.c_void_p)]
+                ("rec_end_step", C.c_void_p), ("ep_code", C.c_void_p), ("applied_act", C.c_void_p),
+                ("dyn_noise_tape", C.c_void_p), ("obs_noise_tape", C.c_void_p)]
 
 
 class PgHeadsArgs(C.Structure):
@@ -124,7 +125,7 @@ class EvalArgs(C.Structure):
                 ("policy_stride", C.c_int64), ("noise_tape", C.c_void_p), ("reset_tape", C.c_void_p),
                 ("policy_seed", C.c_uint64), ("noise_seed", C.c_uint64), ("reset_seed", C.c_uint64)] + \
                [(k, C.c_void_p) for k in ("ep_return", "ep_length", "ep_success", "ep_contacts", "contact_hist",
-                                          "policy_used", "status", "obs_traj", "act_traj")]
+                                          "policy_used", "status", "obs_traj", "act_traj", "work_queue")]
 
 
 _P = C.c_void_p

@@ -626,13 +626,13 @@ extern "C" int dxrl_evaluate(dxrl_env* env, const dxrl_eval_args* args, void* st
             hipLaunchKernelGGL(k_eval<false>, grid, block, 0, st, env->curricula, p);
         return launch_check("k_eval");
     }
-    // k_eval_ls: rows of 16 lanes over a work queue (one counter per device, zeroed on the stream)
-    static int32_t* queues[64] = {nullptr};
+    // k_eval_ls: rows of 16 lanes over a work queue.  The counter is the caller's scratch
+    // (a.work_queue), zeroed on the launch stream: no state shared between launches, so
+    // evaluations on different streams / handles / threads cannot reset each other's queue.
+    DXRL_REQUIRE(a.work_queue, "null work_queue (device i32[1] scratch of this launch)");
     const int dev = env->device;
     DXRL_REQUIRE(dev >= 0 && dev < 64, "device index out of range");
-    if (!queues[dev])
-        if (int rc = hip_check(hipMalloc(&queues[dev], sizeof(int32_t)), "eval queue")) return rc;
-    if (int rc = hip_check(hipMemsetAsync(queues[dev], 0, sizeof(int32_t), st), "eval queue reset")) return rc;
+    if (int rc = hip_check(hipMemsetAsync(a.work_queue, 0, sizeof(int32_t), st), "eval queue reset")) return rc;
     const void* fn = tape ? reinterpret_cast<const void*>(k_eval_ls<true>) : reinterpret_cast<const void*>(k_eval_ls<false>);
     int per_cu = 0, cus = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kEvalThreads, 0);
@@ -649,10 +649,10 @@ extern "C" int dxrl_evaluate(dxrl_env* env, const dxrl_eval_args* args, void* st
     }
     if (tape)
         hipLaunchKernelGGL(k_eval_ls<true>, dim3((unsigned)blocks), dim3(kEvalThreads), 0, st, env->curricula, p,
-                           queues[dev]);
+                           a.work_queue);
     else
         hipLaunchKernelGGL(k_eval_ls<false>, dim3((unsigned)blocks), dim3(kEvalThreads), 0, st, env->curricula, p,
-                           queues[dev]);
+                           a.work_queue);
     if (int rc = launch_check("k_eval_ls")) return rc;
     if (p.diag_iters) {
         unsigned long long it = 0;

@@ -81,8 +81,11 @@ struct PgRolloutArgs {
     int32_t* rec_end_step;
     uint16_t* ep_code;   // [T N] scheduler feed: 0, or (episode length << 1) | success (nullable)
     float* applied_act;  // [T N][kActPad] the action the env integrated (nullable; parity checks)
+    float* dyn_noise_tape;  // [T N][kActPad] f32(sigma) * z as added to the action (nullable; ws kernel)
+    float* obs_noise_tape;  // [(T+1) N][kObsNoiseLd] f32(sigma) * z per observation element (nullable)
     unsigned long long* stamps;  // diag & 32 (k_pg_rollout_ls): cycles per step segment
 };
+constexpr int kObsNoiseLd = 48;
 
 constexpr int kTile = 64;           // envs per workgroup
 constexpr int kXs = kIn + 8;        // LDS row strides (bf16) -- conflict-free b128 fragment reads
@@ -1148,6 +1151,15 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
                     DR.on[j][rbase + ln] = nz[h];
                 }
             }
+            if (p.obs_noise_tape) {  // parity tape: the value write_obs_row adds (row ctr - iteration T)
+                const int64_t row = (int64_t)(ctr - p.iteration * (uint64_t)T);
+                float4 v;
+                v.x = 4 * s + 0 < kObs ? p.obs_noise * nz[0] : 0.0f;
+                v.y = 4 * s + 1 < kObs ? p.obs_noise * nz[1] : 0.0f;
+                v.z = 4 * s + 2 < kObs ? p.obs_noise * nz[2] : 0.0f;
+                v.w = 4 * s + 3 < kObs ? p.obs_noise * nz[3] : 0.0f;
+                *reinterpret_cast<float4*>(p.obs_noise_tape + (row * n + i) * kObsNoiseLd + 4 * s) = v;
+            }
         }
     };
     // ---- aux: the dense reward (RS:50-187) and the episode bookkeeping of a finished step
@@ -1321,6 +1333,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             if (dyn_noise) a = clipf(a + p.dyn_noise * DR.dzn[et_tid], -1.0f, 1.0f);
             p.applied_act[m * kActPad + s] = s < kAct ? a : 0.0f;
         }
+        if (p.dyn_noise_tape)  // parity tape: the value env_lane_step adds to the action
+            p.dyn_noise_tape[m * kActPad + s] = (dyn_noise && s < kAct) ? p.dyn_noise * DR.dzn[et_tid] : 0.0f;
     };
 
     // diag & 128: s_memtime segment stamps per step (diagnostics only): env waves into
@@ -1850,7 +1864,11 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                     a->rec_success,
                     a->rec_end_step,
                     a->ep_code,
-                    a->applied_act};
+                    a->applied_act,
+                    a->dyn_noise_tape,
+                    a->obs_noise_tape};
+    DXRL_REQUIRE(!(a->dyn_noise_tape || a->obs_noise_tape) || !(a->obs_fm || (a->diag_flags & (16 | 32 | 64))),
+                 "the noise tapes are written by the default (warp-specialised) rollout kernel only");
     DeviceGuard g(env->device);
     const int64_t n = env->cfg.num_envs;
     if (a->obs_fm || (a->diag_flags & 16)) {  // feature-major tape / A-B reference: the 64-env kernel

@@ -90,7 +90,8 @@ struct FusedArgs {
     bf16* h1_out;   // [rows][kHx] (columns 0..255 written)
     bf16* dh2_out;  // [rows][kH]
     float* part;    // [grid][kPartSize]
-    double* loss;   // [grid][4]
+    double* loss;   // [loss_rows][4]: row b = workgroup b's loss sums, rows >= gridDim.x zeroed
+    int loss_rows;  // the caller's row count (dxrl_pg_fused_args.grid)
     unsigned long long* stamps;  // diag & 8: [grid][waves][16] cycles per segment
 };
 
@@ -789,7 +790,12 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         const int k = tid - 32;
         double s = 0.0;
         for (int t = 0; t < 64 * kHW; ++t) s += lred[t * 4 + k];
-        if ((p.net == 0) == (k != 1)) p.loss[(int64_t)blockIdx.x * 4 + k] = s;
+        if ((p.net == 0) == (k != 1)) {
+            p.loss[(int64_t)blockIdx.x * 4 + k] = s;
+            // rows of workgroups this launch does not have (fewer tiles than the caller's grid):
+            // zeroed, so a sum over all rows never picks up an earlier, larger pass
+            for (int r = blockIdx.x + gridDim.x; r < p.loss_rows; r += gridDim.x) p.loss[(int64_t)r * 4 + k] = 0.0;
+        }
     }
 }
 
@@ -927,6 +933,7 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     f.dh2_out = static_cast<bf16*>(a->dh2);
     f.part = a->partial;
     f.loss = a->loss_partial;
+    f.loss_rows = a->grid;
     // tile geometry: 128-sample tiles, one 8-wave workgroup per CU (160 KiB LDS), or 64-sample
     // tiles, two 4-wave workgroups per CU (80 KiB each) -- DXRL_FUSED_TILE=64|128 (A/B)
     static const int tile = [] {

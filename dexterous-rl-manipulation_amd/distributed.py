@@ -14,6 +14,12 @@ sharded run draws exactly what the same envs draw unsharded.  The PG learner
     gradient of the global-batch mean loss, ragged shards included.
 The curriculum scheduler (config C3) additionally all-gathers each rank's
 episode-end codes so every rank feeds the same global episode stream.
+
+Every helper runs its collective when ``world > 1`` OR a process group is passed:
+a world-1 process group (``bench.py --dist``, tests/test_gpu_rccl.py) executes the
+same RCCL calls a multi-rank job makes, whose results then equal their inputs.
+Per-rank shards must be equal in size (the all-gathers and the scheduler's
+global env ids assume it; PGTrainer checks).
 """
 from __future__ import annotations
 
@@ -58,6 +64,11 @@ def init_from_env(backend: Optional[str] = None) -> Topology:
     return Topology(world, rank, local, dev, group)
 
 
+def _active(world: int, group) -> bool:
+    """Run the collective: several ranks, or an explicit process group (even of one rank)."""
+    return world > 1 or group is not None
+
+
 def _staged(t: torch.Tensor, group) -> bool:
     """gloo process groups (CPU tests, two ranks sharing one test GPU) exchange host copies."""
     import torch.distributed as dist
@@ -65,8 +76,8 @@ def _staged(t: torch.Tensor, group) -> bool:
 
 
 def all_reduce_sum_(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
-    """In-place SUM over ranks (no-op for world == 1)."""
-    if world > 1:
+    """In-place SUM over ranks (no-op for world == 1 without a process group)."""
+    if _active(world, group):
         import torch.distributed as dist
         if _staged(t, group):
             h = t.cpu()
@@ -79,7 +90,7 @@ def all_reduce_sum_(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
 
 def all_gather_into_(out: torch.Tensor, t: torch.Tensor, world: int, group=None) -> torch.Tensor:
     """out[r * t.numel():(r + 1) * t.numel()] = rank r's t (one collective; rank-major)."""
-    if world == 1:
+    if not _active(world, group):
         if out.data_ptr() != t.data_ptr():
             out.view(-1).copy_(t.view(-1))
         return out
@@ -133,7 +144,7 @@ def loss_scales(global_samples: int, world: int, ent_coef: float) -> tuple:
 
 def global_count(local: int, world: int, group=None) -> int:
     """SUM of a per-rank integer (one-time, at trainer construction)."""
-    if world == 1:
+    if not _active(world, group):
         return int(local)
     t = torch.tensor([int(local)], dtype=torch.int64)
     import torch.distributed as dist
@@ -144,7 +155,7 @@ def global_count(local: int, world: int, group=None) -> int:
 
 
 def all_reduce_max(x: float, world: int, device, group=None) -> float:
-    if world == 1:
+    if not _active(world, group):
         return x
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64, device=device)
@@ -153,7 +164,7 @@ def all_reduce_max(x: float, world: int, device, group=None) -> float:
 
 
 def barrier(world: int, group=None):
-    if world > 1:
+    if _active(world, group):
         import torch.distributed as dist
         dist.barrier(group=group)
 

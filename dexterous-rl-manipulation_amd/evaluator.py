@@ -257,6 +257,15 @@ class EpisodeProgram:
             repeat: int = 1, timing: Optional[Dict] = None, trajectories: bool = False) -> EvalRecords:
         """Launch the plan (``repeat`` back-to-back launches; ``timing['kernel_ms']`` =
         HIP-event time per launch on the launch stream)."""
+        return self.launch(prog, policy_tapes, host_resets, host_noise, device_seed, keep_history, repeat,
+                           trajectories).result(timing)
+
+    def launch(self, prog: _PolicyProgram, policy_tapes: Optional[np.ndarray] = None, host_resets: bool = True,
+               host_noise: bool = True, device_seed: int = 0, keep_history: bool = True, repeat: int = 1,
+               trajectories: bool = False, stream: Optional[torch.cuda.Stream] = None) -> "_PendingRun":
+        """Enqueue the plan on ``stream`` (default: the device's current stream) without waiting;
+        ``.result()`` synchronises and returns the records.  Every launch owns its buffers,
+        including the work-queue counter, so launches on different streams may overlap."""
         plan = self.plan(host_resets, host_noise)
         dev = self.device = N.require_gpu(self.device)
         nl, E = len(self.lanes), plan.total_episodes
@@ -282,6 +291,7 @@ class EpisodeProgram:
         o_traj = torch.zeros(E, ms + 1, OBS_DIM, dtype=torch.float32, device=dev) if trajectories else None
         a_traj = torch.zeros(E, ms, ACTION_DIM, dtype=torch.float32, device=dev) if trajectories else None
         status = torch.zeros(1, dtype=torch.int32, device=dev)
+        queue = torch.zeros(1, dtype=torch.int32, device=dev)  # this launch's work-queue counter
         a = N.EvalArgs()
         a.num_lanes, a.policy, a.max_steps, a.total_episodes = nl, prog.kind, ms, E
         a.lane_segments, a.segments, a.mean_action = N.ptr(d_lane), N.ptr(d_seg), N.ptr(mean)
@@ -293,27 +303,19 @@ class EpisodeProgram:
         a.ep_return, a.ep_length, a.ep_success = N.ptr(out_ret), N.ptr(out_len), N.ptr(out_suc)
         a.ep_contacts, a.contact_hist = N.ptr(out_con), N.ptr(out_hist)
         a.policy_used, a.status = N.ptr(used), N.ptr(status)
-        a.obs_traj, a.act_traj = N.ptr(o_traj), N.ptr(a_traj)
+        a.obs_traj, a.act_traj, a.work_queue = N.ptr(o_traj), N.ptr(a_traj), N.ptr(queue)
         with torch.cuda.device(dev):
-            st = torch.cuda.current_stream(dev)
+            st = stream if stream is not None else torch.cuda.current_stream(dev)
+            # the inputs were written on the current stream; the launch stream waits for them
+            st.wait_stream(torch.cuda.current_stream(dev))
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             for _ in range(max(1, int(repeat))):
-                N.call("dxrl_evaluate", env.handle, C.byref(a), env._stream())
+                N.call("dxrl_evaluate", env.handle, C.byref(a), st.cuda_stream)
             e1.record(st)
-            st.synchronize()
-            if timing is not None:
-                timing["kernel_ms"] = e0.elapsed_time(e1) / max(1, int(repeat))
-        if int(status.item()):
-            raise N.NativeError("dxrl_evaluate: a parity tape ran out or a segment was malformed")
-        env.close()
-        p = plan.props
-        return EvalRecords(out_ret.cpu().numpy(), out_len.cpu().numpy(), out_suc.cpu().numpy().astype(bool),
-                           out_con.cpu().numpy(),
-                           out_hist.cpu().numpy() if keep_history else np.zeros((E, 0), np.uint8),
-                           p[:, 0], p[:, 1], p[:, 2], used.cpu().numpy(),
-                           o_traj.cpu().numpy() if trajectories else None,
-                           a_traj.cpu().numpy() if trajectories else None)
+        keep = (env, a, d_lane, d_seg, mean, d_pol, d_noise, d_reset, queue)  # alive until the stream is done
+        return _PendingRun(st, e0, e1, max(1, int(repeat)), status, plan.props, keep_history, trajectories,
+                           (out_ret, out_len, out_suc, out_con, out_hist, used, o_traj, a_traj), keep, E)
 
 
     def run_facade(self, policy, trajectories: bool = False) -> EvalRecords:
@@ -377,6 +379,31 @@ class ProgramPlan:
     props: np.ndarray             # f64 [E][3] size, mass, friction of each episode (NaN: device-drawn)
     noise: Optional[np.ndarray]   # f64 standard normals or None (device Philox noise)
     total_episodes: int
+
+
+class _PendingRun:
+    """An enqueued dxrl_evaluate launch (EpisodeProgram.launch); result() waits for its stream."""
+
+    def __init__(self, stream, e0, e1, repeat, status, props, keep_history, trajectories, outs, keep, E):
+        self.stream, self.e0, self.e1, self.repeat = stream, e0, e1, repeat
+        self.status, self.props, self.keep_history, self.trajectories = status, props, keep_history, trajectories
+        self.outs, self.keep, self.E = outs, keep, E
+
+    def result(self, timing: Optional[Dict] = None) -> EvalRecords:
+        self.stream.synchronize()
+        if timing is not None:
+            timing["kernel_ms"] = self.e0.elapsed_time(self.e1) / self.repeat
+        if int(self.status.item()):
+            raise N.NativeError("dxrl_evaluate: a parity tape ran out or a segment was malformed")
+        self.keep[0].close()
+        out_ret, out_len, out_suc, out_con, out_hist, used, o_traj, a_traj = self.outs
+        p = self.props
+        return EvalRecords(out_ret.cpu().numpy(), out_len.cpu().numpy(), out_suc.cpu().numpy().astype(bool),
+                           out_con.cpu().numpy(),
+                           out_hist.cpu().numpy() if self.keep_history else np.zeros((self.E, 0), np.uint8),
+                           p[:, 0], p[:, 1], p[:, 2], used.cpu().numpy(),
+                           o_traj.cpu().numpy() if self.trajectories else None,
+                           a_traj.cpu().numpy() if self.trajectories else None)
 
 
 def _exact_tape(prog: _PolicyProgram, program: EpisodeProgram) -> np.ndarray:

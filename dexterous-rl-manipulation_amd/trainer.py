@@ -112,9 +112,17 @@ class PGTrainer:
         if (cfg.epochs > 1 or cfg.minibatches > 1) and not cfg.fused:
             raise ValueError("epochs / minibatches need the fused learner")
         self._mb = (0, self.M)  # (first sample, samples) of the minibatch the train passes read
+        self._loss_rows = self.M  # rows of the last train pass (loss_stats)
         self.pg = process_group
         self.world = world_size
+        # collectives run with several ranks or with an explicit process group (a world-1 group
+        # executes the same RCCL calls: bench.py --dist, tests/test_gpu_rccl.py)
+        self.collective = process_group is not None or world_size > 1
         self.global_M = global_count(self.M, self.world, self.pg)  # samples of all ranks per iteration
+        if self.global_M != self.M * self.world:
+            raise ValueError(f"every rank needs the same num_envs * horizon ({self.M} here, {self.global_M} over "
+                             f"{self.world} ranks): the episode-code all-gather and the scheduler's global env ids "
+                             "assume equal shards")
         self.step_count = 0
         self.iteration_index = 0
         self.diag_flags = 0  # rollout timing ablations only (see dxrl_pg_rollout_args.diag_flags)
@@ -145,21 +153,30 @@ class PGTrainer:
         # hidden activations, row-major [rows][288]: columns 0..255 = tanh units, column 256 = 1
         # (the next layer reads K = 256; the weight-gradient GEMM reads I = 288 and gets the bias
         # gradient as column 256)
-        self.H1a, self.H2a = z(M, HX, dt=bf), z(M, HX, dt=bf)
-        self.H1c, self.H2c = z((T + 1) * n, HX, dt=bf), z((T + 1) * n, HX, dt=bf)
-        for t in (self.H1a, self.H2a, self.H1c, self.H2c):
-            t[:, H].fill_(1.0)
-        self.mu = z(M, OUT)
-        self.V = z(OUT, (T + 1) * n)
+        # The layer-by-layer GEMM chain (fused=False, the A/B path) stores every activation and
+        # head gradient; the fused learner keeps them on chip and needs only dH2 (and H1 in
+        # H1-copy mode), so nothing else is allocated for it (C4: ~5 GB less).
+        chain = not cfg.fused
+        self.H1a = z(M, HX, dt=bf) if chain or not cfg.h1_recompute else None
+        self.H2a = self.H1c = self.H2c = self.mu = self.dmu_rm = self.dv_rm = self.dH1 = None
+        self.dls_partial = self.loss_partial = None
+        if chain:
+            self.H2a = z(M, HX, dt=bf)
+            self.H1c, self.H2c = z((T + 1) * n, HX, dt=bf), z((T + 1) * n, HX, dt=bf)
+            for t in (self.H1a, self.H2a, self.H1c, self.H2c):
+                t[:, H].fill_(1.0)
+            self.mu = z(M, OUT)
+            self.dmu_rm, self.dv_rm = z(M, OUT, dt=bf), z(M, OUT, dt=bf)
+            self.dls_partial = z((M + 255) // 256, ACT_PAD)
+            self.loss_partial = torch.zeros((M + 255) // 256, 4, dtype=torch.float64, device=d)
+            self.dH1 = z(M, H, dt=bf)
+        self.V = z(OUT if chain else 1, (T + 1) * n)  # the GEMM chain writes all 32 head rows
         self.adv, self.ret = z(M), z(M)
         self.stats = torch.zeros(8, dtype=torch.float64, device=d)
         self.moments_all = torch.zeros(self.world, 3, dtype=torch.float64, device=d)  # ranks' stats[5..7]
         nb = max(1024, (M + 255) // 256, 3 * ((n + 63) // 64))  # GAE: one (n, mean, M2) per 64-env block
         self.partial = torch.zeros(nb, dtype=torch.float64, device=d)
-        self.dmu_rm, self.dv_rm = z(M, OUT, dt=bf), z(M, OUT, dt=bf)
-        self.dls_partial = z((M + 255) // 256, ACT_PAD)
-        self.loss_partial = torch.zeros((M + 255) // 256, 4, dtype=torch.float64, device=d)
-        self.dH2, self.dH1 = z(M, H, dt=bf), z(M, H, dt=bf)
+        self.dH2 = z(M, H, dt=bf)
         self.splits = max(1, min(cfg.splitk_target_blocks // 3, M // 1024))  # dW2: one workgroup per CU
         self.kpartial = z(self.splits + 16, H, HX)  # + two-level reduction scratch
         self.gnorm2 = torch.zeros(1, dtype=torch.float64, device=d)
@@ -229,7 +246,9 @@ class PGTrainer:
         a.rec_return, a.rec_length = p(self.rec_return), p(self.rec_length)
         a.rec_success, a.rec_end_step = p(self.rec_success), p(self.rec_end)
         a.ep_code = p(self.ep_code)
-        a.applied_act = p(getattr(self, "applied_act", None))
+        a.applied_act = p(getattr(self, "applied_act", None))  # parity tapes (tests only; None in runs)
+        a.dyn_noise_tape = p(getattr(self, "dyn_noise_tape", None))
+        a.obs_noise_tape = p(getattr(self, "obs_noise_tape", None))
         N.call("dxrl_pg_rollout", self.env.handle, p(self.packed), p(self.params), C.byref(a), self._s())
 
     def _mlp_forward(self, net, rows, H1, H2, head_f32=None, head_fm=None, ld_head_fm=0):
@@ -256,9 +275,9 @@ class PGTrainer:
         f.act, f.logp_old, f.adv, f.ret = p(self.act[start:]), p(self.logp[start:]), p(self.adv[start:]), \
             p(self.ret[start:])
         f.stats = p(self.stats)
-        # each minibatch is one gradient step on the mean loss over its samples of all ranks
-        f.inv_total_samples, f.ent_coef = loss_scales(self.global_M // self.cfg.minibatches, self.world,
-                                                      c.ent_coef)
+        # each pass is one gradient step on the mean loss over its samples of all ranks (equal
+        # shards: rows per rank x world)
+        f.inv_total_samples, f.ent_coef = loss_scales(rows * self.world, self.world, c.ent_coef)
         f.clip_eps, f.vf_coef = c.clip_eps, c.vf_coef
         f.values = p(self.V[0])
         f.h1, f.dh2 = p(self.H1a), p(self.dH2)
@@ -273,10 +292,12 @@ class PGTrainer:
 
     def actor_train(self):
         start, rows = self._mb
+        self._loss_rows = rows
         N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(0, True, rows, start)), self._s())
 
     def critic_train(self):
         start, rows = self._mb
+        self._loss_rows = rows
         N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(1, True, rows, start)), self._s())
 
     def ppo_updates(self):
@@ -315,7 +336,7 @@ class PGTrainer:
                c.gamma, c.lam, N.ptr(self.adv), N.ptr(self.ret), N.ptr(self.partial), N.ptr(self.stats), self._s())
         # every rank's (count, mean, M2) in rank order, merged on device (identical on all ranks);
         # one rank: dxrl_pg_gae already wrote the combined statistics
-        if self.world > 1:
+        if self.collective:
             gather_adv_moments_(self.moments_all, self.stats, self.world, self.pg)
             N.call("dxrl_pg_adv_combine", self.dev.index, N.ptr(self.moments_all), self.world, N.ptr(self.stats),
                    self._s())
@@ -369,8 +390,8 @@ class PGTrainer:
         self.env.set_curriculum(scheduler.get_current_config())
         d, n, T = self.dev, self.n, self.T
         self.ep_code = torch.zeros(T * n, dtype=torch.int16, device=d)
-        self.codes_all = self.ep_code if self.world == 1 else torch.zeros(self.world * T * n, dtype=torch.int16,
-                                                                          device=d)
+        self.codes_all = self.ep_code if not self.collective else torch.zeros(self.world * T * n, dtype=torch.int16,
+                                                                              device=d)
         w = max(1, int(scheduler.window_size))
         self._sched_w = w
         self._tail_dev = torch.zeros(2, w, dtype=torch.int16, device=d)
@@ -477,8 +498,9 @@ class PGTrainer:
         return out
 
     def loss_stats(self) -> Dict[str, float]:
-        """Loss terms of the last train pass (the last minibatch of the last epoch)."""
-        rows = self.M // self.cfg.minibatches
+        """Loss terms of the last train pass (the last minibatch of the last epoch), per sample of
+        that pass (the fused kernel zeroes the loss rows of workgroups a pass did not launch)."""
+        rows = self._loss_rows if self.cfg.fused else self.M
         s = (self.fused_loss if self.cfg.fused else self.loss_partial).sum(0).cpu().numpy() / rows
         return {"policy_loss": float(s[0]), "value_mse": float(s[1]), "clip_frac": float(s[2]),
                 "approx_kl": float(s[3]), "grad_norm": float(np.sqrt(self.gnorm2.item()))}

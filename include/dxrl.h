@@ -262,6 +262,12 @@ typedef struct dxrl_pg_rollout_args {
                                   (episode length << 1) | success (nullable)                  */
     float* applied_act;        /* f32 [T N][16] the action the env integrated, after dynamics
                                   noise (nullable; parity checks replay it on the CPU)        */
+    /* Fused-noise tapes (config C5; nullable, parity checks only; default kernel only): the
+       f32 noise values exactly as the kernel added them, n = f32(sigma) * z with z the
+       device's Box-Muller normal -- robustness_tests.py:180-182 draws n = N(0, sigma) and
+       adds f32(n) to the action; :199-207 adds f32(n) to every observation element. */
+    float* dyn_noise_tape;     /* f32 [T N][16] dynamics noise per action dim (0 if off)    */
+    float* obs_noise_tape;     /* f32 [(T+1) N][48] observation noise per obs element       */
 } dxrl_pg_rollout_args;
 
 /* Fused policy + env rollout: T steps of actor MLP (bf16 MFMA) -> Gaussian
@@ -453,6 +459,10 @@ typedef struct dxrl_eval_args {
        action of every step.  Rows past an episode's length are left untouched. */
     float* obs_traj;
     float* act_traj;
+    /* device i32 [1] scratch owned by the caller: this launch's work-queue counter (zeroed on
+       the stream by the call).  Required by the default (work-queue) kernel; give each launch
+       that may run concurrently with another its own counter. */
+    int32_t* work_queue;
 } dxrl_eval_args;
 
 int dxrl_evaluate(dxrl_env* env, const dxrl_eval_args* args, void* stream);

@@ -400,3 +400,41 @@ def philox_reset_draws(cur: OracleCurriculum, k0: int, k1: int, ctr: int) -> np.
     for k, rg in enumerate(rngs):
         d[D + k] = math.nan if rg is None else rg[0] + (rg[1] - rg[0]) * u[D + k]
     return d
+
+
+# ---------------------------------------------------------------- device noise streams (config C5)
+STREAM_POLICY, STREAM_DYN, STREAM_OBS = 0x504F4C00, 0x44594E00, 0x4F425300  # csrc/dxrl_device.h kStream*
+
+
+def philox4x32_10_np(c0, c1, c2, c3, k0, k1):
+    """Vectorised philox4x32_10 over NumPy arrays (uint64 lanes holding u32 values)."""
+    m = np.uint64(_U32)
+    x, y, z, w = (np.asarray(v, np.uint64) & m for v in (c0, c1, c2, c3))
+    k0 = np.asarray(k0, np.uint64) & m
+    k1 = np.asarray(k1, np.uint64) & m
+    for _ in range(10):
+        p0, p1 = np.uint64(_PH_M0) * x, np.uint64(_PH_M1) * z
+        x, y, z, w = ((p1 >> np.uint64(32)) ^ y ^ k0) & m, p1 & m, ((p0 >> np.uint64(32)) ^ w ^ k1) & m, p0 & m
+        k0, k1 = (k0 + np.uint64(_PH_W0)) & m, (k1 + np.uint64(_PH_W1)) & m
+    return x, y, z, w
+
+
+def device_normals_f64(key, ctr, stream: int, blocks: int) -> np.ndarray:
+    """The device's Box-Muller normals (csrc/dxrl_device.h box_muller over u01_24 of one
+    Philox block: block b gives normals 4b .. 4b+3 = (r cos, r sin) of (x, y), then of (z, w)),
+    restated in f64 with libm.  The device evaluates them with hardware log / sqrt / sin / cos
+    in f32, so the values agree to ~1e-6 relative, not bit for bit: the tests use this to pin
+    WHICH draws (key, counter, stream, block) a kernel consumed.  ``ctr``: uint64 array;
+    ``key``: (k0, k1) arrays broadcastable to it.  Returns f64 [..., 4 * blocks]."""
+    ctr = np.asarray(ctr, np.uint64)
+    out = []
+    for b in range(blocks):
+        x, y, z, w = philox4x32_10_np(ctr & np.uint64(_U32), ctr >> np.uint64(32), np.full(ctr.shape, stream),
+                                      np.full(ctr.shape, b), key[0], key[1])
+        for a_, b_ in ((x, y), (z, w)):
+            ua = ((a_ >> np.uint64(8)).astype(np.float64) + 1.0) * (1.0 / 16777216.0)
+            ub = ((b_ >> np.uint64(8)).astype(np.float64) + 1.0) * (1.0 / 16777216.0)
+            r = np.sqrt(-2.0 * np.log(ua))
+            ang = 6.283185307179586 * ub
+            out += [r * np.cos(ang), r * np.sin(ang)]
+    return np.stack(out, axis=-1)

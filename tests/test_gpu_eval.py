@@ -279,3 +279,36 @@ def test_lane_split_eval_matches_one_lane_kernel(policy, noise, traj, monkeypatc
         for i, n in enumerate(a.ep_length.astype(int)):
             assert np.array_equal(a.obs_traj[i, :n + 1], b.obs_traj[i, :n + 1]), i
             assert np.array_equal(a.act_traj[i, :n], b.act_traj[i, :n]), i
+
+
+def test_concurrent_evaluations_on_two_streams(monkeypatch):
+    """Two evaluations enqueued on two streams before either finishes (each launch owns its
+    work-queue counter, dxrl_eval_args.work_queue) give exactly what the CPU oracle and the
+    one-lane kernel give for each plan alone: a shared queue counter would let one launch's
+    reset re-issue or skip the other's program lanes."""
+    rng = np.random.default_rng(31)
+    runs = []
+    for k, (cfg, noise) in enumerate((("variable", (0.05, 0.1)), ("hard", (0.0, 0.0)))):
+        pol = make_policy("simple", rng.uniform(-0.5, 0.5, 15).astype(np.float32), 5 + k)
+        prog = evr.policy_program(pol)
+        p = evr.EpisodeProgram([cfg_of(cfg), cfg_of("easy")], "dense", max_episode_steps=120, max_steps=100)
+        for lane in range(250 + 50 * k):
+            o, d = noise if rng.random() < 0.5 else (0.0, 0.0)
+            p.add_lane([evr.Segment(int(rng.integers(0, 2)), [int(rng.integers(0, 10**6))], o, d,
+                                    noise_seed=int(rng.integers(0, 10**6)))])
+        need = max(sum(len(s.episode_seeds) for s in lane) for lane in p.lanes) * p.max_steps * 15
+        tapes = np.stack([prog.seeded(int(s), need) for s in rng.integers(0, 10**6, len(p.lanes))])
+        runs.append((p, prog, tapes))
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    pending = [p.launch(prog, policy_tapes=tapes, repeat=3, stream=s) for (p, prog, tapes), s in zip(runs, streams)]
+    got = [x.result() for x in pending]
+    monkeypatch.setenv("DXRL_EVAL_ONE_LANE", "1")
+    for (p, prog, tapes), rec in zip(runs, got):
+        one = p.run(prog, policy_tapes=tapes)
+        want = run_oracle(p, prog, tapes)
+        for k in ("ep_length", "ep_success", "ep_contacts", "contact_hist", "policy_used"):
+            assert np.array_equal(getattr(rec, k), getattr(one, k)), k
+            assert np.array_equal(getattr(rec, k), getattr(want, k)), k
+        assert np.array_equal(rec.ep_return, one.ep_return)
+        np.testing.assert_allclose(rec.ep_return, want.ep_return, rtol=1e-12, atol=1e-15)

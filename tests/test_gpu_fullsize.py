@@ -8,8 +8,10 @@ held-out table 8192x200, C5 variable + noise 0.05 4096x200), each checked three 
    pg_reference.gae must give the kernel's adv / ret to 1e-5 (north star), and the
    one-pass f64 mean / std must equal a two-pass f64 reduction of the kernel's adv;
 3. the rollout tape: >= 32 lanes (first, last, every 16-env workgroup boundary probed,
-   random) replayed for all 200 steps by the CPU oracle -- actions from the applied-action
-   tape, auto-resets from the oracle's Philox restatement -- rewards / dones / obs equal.
+   random) replayed for all 200 steps by the CPU oracle -- the oracle's own noisy action /
+   observation from the policy action and the noise values the kernel drew (config C5),
+   auto-resets from the oracle's Philox restatement -- applied actions / rewards / dones /
+   obs equal; the noise values themselves pinned to their Philox draws and moments.
 
 Reference analogue: the returns of training/episode_utils.py:42-53 (the reference has no
 GAE or network learner: parity of the learner itself is unpinned)."""
@@ -20,10 +22,16 @@ import pytest
 import torch
 
 import pg_reference as R
-from oracle.dx_oracle import OracleCurriculum, OracleEnv, env_key, philox_reset_draws
+from oracle.dx_oracle import (STREAM_DYN, STREAM_OBS, OracleCurriculum, OracleEnv, device_normals_f64, env_key,
+                              oracle_noisy_action, oracle_noisy_obs, philox_reset_draws)
 
 pytestmark = pytest.mark.gpu
 CONFIGS = ["easy", "default", "hard_heldout", "variable_noise"]
+
+
+def env_key_np(seed, gid):
+    k = [env_key(seed, int(g)) for g in gid]
+    return np.array([a for a, _ in k], np.uint64), np.array([b for _, b in k], np.uint64)
 
 
 @pytest.fixture(scope="module")
@@ -37,6 +45,8 @@ def _run(pkg, name, **kw):
     dev = torch.device("cuda", 0)
     env, tr = pkg.workloads.build_pg_workload(name, dev, ent_coef=0.01, **kw)
     tr.applied_act = torch.zeros(tr.M, 16, device=dev)
+    tr.dyn_noise_tape = torch.full((tr.M, 16), float("nan"), device=dev)
+    tr.obs_noise_tape = torch.full((tr.M + tr.n, 48), float("nan"), device=dev)
     st0 = {k: getattr(env, k).clone() for k in ("joint_positions", "object_position", "object_size", "object_mass",
                                                  "friction_coefficient", "curriculum_index", "reset_counter")}
     st0["curricula"] = list(env.curriculum_configs)  # C3: a progression swaps the table after the iteration
@@ -106,18 +116,34 @@ def test_gae_and_normalisation_isolated(run):
 
 
 def test_rollout_tape_matches_oracle(run):
+    """>= 32 lanes replayed by the oracle for all 200 steps.  The oracle steps with the action
+    IT derives from the policy's tape action and the dynamics noise the kernel drew:
+    clip(f32(a + f32(n)), -1, 1) (oracle_noisy_action, robustness_tests.py:177-187), which must
+    equal the action the kernel integrated (applied_act) bit for bit; every observation row must
+    equal bf16(f32(obs + f32(n_obs))) (oracle_noisy_obs, robustness_tests.py:199-207) with the
+    observation noise the kernel drew.  Without noise the same check runs with n = 0."""
     name, env, tr, st0 = run
     n, T = tr.n, tr.T
     rew, done = tr.rew.view(T, n).cpu().numpy(), tr.done.view(T, n).cpu().numpy()
-    act = tr.applied_act.view(T, n, 16).cpu().numpy()
+    applied = tr.applied_act.view(T, n, 16).cpu().numpy()
+    pol_act = tr.act.view(T, n, 16).cpu().numpy()
+    nd = tr.dyn_noise_tape.view(T, n, 16).cpu().numpy()
+    no = tr.obs_noise_tape.view(T + 1, n, 48).cpu().numpy()
     obs = tr.obs_rm.view(T + 1, n, 64).float().cpu().numpy()
     s = {k: v.cpu().numpy() for k, v in st0.items() if k != "curricula"}
     curs = [_oracle_cur(c) for c in st0["curricula"]]
     seed = env._cfg.seed
-    noisy_obs = tr.cfg.obs_noise_std > 0
+    dyn_on, obs_on = tr.cfg.dyn_noise_std > 0, tr.cfg.obs_noise_std > 0
+    if not dyn_on:
+        assert not nd.any()
     lanes = _lanes(n)
     assert len(lanes) >= 32
     resets = 0
+    bf = lambda x: torch.from_numpy(np.asarray(x, np.float32)).to(torch.bfloat16).float().numpy()  # noqa: E731
+
+    def want_row(ob, t, i):
+        return bf(oracle_noisy_obs(np.asarray(ob, np.float32), no[t, i, :45]) if obs_on else ob)
+
     for i in lanes:
         cur = curs[int(s["curriculum_index"][i])]
         orc = OracleEnv(cur=cur, dense=True, max_episode_steps=env.max_episode_steps)
@@ -129,10 +155,12 @@ def test_rollout_tape_matches_oracle(run):
         k0, k1 = env_key(seed, env._cfg.global_env_offset + i)
         ctr = int(s["reset_counter"][i]) & ((1 << 64) - 1)
         for t in range(T):
-            if not noisy_obs:
-                want = torch.from_numpy(np.asarray(ob, np.float32)).to(torch.bfloat16).float().numpy()
-                assert np.array_equal(obs[t, i, :45], want), (name, i, t)
-            ob, r, te, trn = orc.step(act[t, i, :15])
+            assert np.array_equal(obs[t, i, :45], want_row(ob, t, i)), (name, i, t)
+            a = pol_act[t, i, :15]
+            if dyn_on:
+                a = np.asarray(oracle_noisy_action(a, nd[t, i, :15]), np.float32)
+            assert np.array_equal(applied[t, i, :15], a), (name, i, t)
+            ob, r, te, trn = orc.step(a)
             r32 = np.float32(r)
             assert abs(rew[t, i] - r32) <= np.spacing(abs(r32)), (name, i, t, rew[t, i], r)
             d_ = te or trn or orc.t >= tr.max_steps
@@ -141,10 +169,46 @@ def test_rollout_tape_matches_oracle(run):
                 ob = orc.reset(philox_reset_draws(cur, k0, k1, ctr))
                 ctr += 1
                 resets += 1
-        if not noisy_obs:
-            want = torch.from_numpy(np.asarray(ob, np.float32)).to(torch.bfloat16).float().numpy()
-            assert np.array_equal(obs[T, i, :45], want), (name, i, "bootstrap")
+        assert np.array_equal(obs[T, i, :45], want_row(ob, T, i)), (name, i, "bootstrap")
     assert resets > 0
+
+
+def test_fused_noise_streams(run):
+    """Config C5's noise as drawn: the dynamics / observation noise tapes hold f32(sigma) * z
+    with z the Box-Muller normal of the lane's own Philox block (policy key of the global env
+    id, counter iteration * T + t, the dyn / obs stream, block = element // 4) -- checked
+    against the oracle's f64 restatement of those draws on the sampled lanes (hardware
+    log / sqrt / sin / cos: ~1e-6 relative, so this pins WHICH draws were added, the exact
+    arithmetic applied to them is test_rollout_tape_matches_oracle's) -- and their moments over
+    the whole 4096 x 200 tape (mean 0, std sigma).  The reference draws n = N(0, sigma) in f64
+    and rounds to f32 (robustness_tests.py:181-182, :203-204); the kernel rounds sigma to f32
+    and multiplies in f32."""
+    name, env, tr, _ = run
+    c = tr.cfg
+    if c.dyn_noise_std <= 0 and c.obs_noise_std <= 0:
+        pytest.skip("no fused noise in this workload")
+    n, T = tr.n, tr.T
+    nd = tr.dyn_noise_tape.view(T, n, 16).double().cpu().numpy()
+    no = tr.obs_noise_tape.view(T + 1, n, 48).double().cpu().numpy()
+    assert not np.isnan(nd).any() and not np.isnan(no).any()
+    assert not nd[:, :, 15:].any() and not no[:, :, 45:].any()
+    pseed = (int(c.seed) * 0x9E3779B97F4A7C15 + 17) & (2**64 - 1)
+    lanes = np.array(_lanes(n))
+    gid = env._cfg.global_env_offset + lanes
+    key = env_key_np(pseed, gid)
+    for sig, tape, stream, blocks, rows, width in ((c.dyn_noise_std, nd, STREAM_DYN, 4, T, 15),
+                                                   (c.obs_noise_std, no, STREAM_OBS, 12, T + 1, 45)):
+        sig32 = float(np.float32(sig))
+        vals = tape[:, :, :width]
+        N_ = vals.size
+        assert abs(vals.mean()) < 6 * sig / math.sqrt(N_), (name, vals.mean())
+        assert abs(vals.std() / sig - 1.0) < 2e-3, (name, vals.std())
+        ctr = (np.uint64(tr.iteration_index) * np.uint64(T) + np.arange(rows, dtype=np.uint64))[:, None]
+        ctr = np.broadcast_to(ctr, (rows, len(lanes)))
+        z = device_normals_f64((key[0][None, :], key[1][None, :]), ctr, stream, blocks)[..., :width]
+        got = vals[:rows][:, lanes]
+        err = np.abs(got - sig32 * z)
+        assert (err <= sig32 * (1e-4 + 1e-4 * np.abs(z))).all(), (name, stream, err.max())
 
 
 def test_normalisation_large_mean(pkg):

@@ -326,28 +326,31 @@ def test_lane_split_rollout_matches_64_env_kernel(pkg, cur, n, noise):
 
 
 def test_minibatch_gradients_sum_to_full_batch(pkg):
-    """Time-contiguous minibatches (pointer offsets into the tape, same kernels): the two
-    halves' gradients sum to the full batch's under the same per-sample scale."""
+    """Time-contiguous minibatches (pointer offsets into the tape, same kernels): each pass is
+    the gradient of the mean loss over its own samples (scale 1 / its rows), so the mean of the
+    two halves' gradients equals the full batch's -- log_std included (its entropy bonus
+    enters every pass once) -- and loss_stats() of each pass is per sample of that pass."""
     env, tr = make(pkg, 256, 32, minibatches=2)
     for name in ("rollout", "critic_values", "advantages"):
         getattr(tr, name)()
     M = tr.M
-    got = []
+    got, losses = [], []
     for mb in ((0, M // 2), (M // 2, M // 2), (0, M)):
         tr._mb = mb
         tr.actor_train()
         tr.critic_train()
         torch.cuda.synchronize()
         got.append(tr.grads.clone())
+        losses.append(tr.loss_stats())
     T_ = pkg.trainer
     ls = slice(T_.OFF["logstd"], T_.OFF["logstd"] + 15)
     for name in ("W1a", "W2a", "W3a", "W1c", "W2c", "W3c"):
-        a = tr.block(name, got[0]) + tr.block(name, got[1])
+        a = 0.5 * (tr.block(name, got[0]) + tr.block(name, got[1]))
         b = tr.block(name, got[2])
         assert ((a - b).norm() / b.norm()).item() < 1e-5, name
-    # log_std: the entropy bonus enters every launch once (ent_coef / world)
-    ent = tr.cfg.ent_coef
-    torch.testing.assert_close(got[0][ls] + got[1][ls] + ent, got[2][ls], rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(0.5 * (got[0][ls] + got[1][ls]), got[2][ls], rtol=1e-5, atol=1e-7)
+    for k in ("policy_loss", "value_mse"):
+        assert abs(0.5 * (losses[0][k] + losses[1][k]) - losses[2][k]) <= 1e-5 * max(1.0, abs(losses[2][k])), k
 
 
 def test_ppo_epochs_engage_the_clip(pkg):

@@ -136,3 +136,28 @@ def test_philox_known_answers():
             (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
     for ctr, key, want in kat:
         assert philox4x32_10(ctr, key) == want
+
+
+def test_vectorised_philox_matches_scalar():
+    """philox4x32_10_np (the full-size C5 noise checks) == the KAT-pinned scalar restatement,
+    and device_normals_f64 follows the block / half / (cos, sin) order of box_muller."""
+    import math
+    from oracle.dx_oracle import _U32, device_normals_f64, philox4x32_10, philox4x32_10_np
+    rng = np.random.default_rng(3)
+    c = rng.integers(0, 2**32, (4, 64), dtype=np.uint64)
+    k = rng.integers(0, 2**32, (2, 64), dtype=np.uint64)
+    got = philox4x32_10_np(*c, *k)
+    for j in range(64):
+        want = philox4x32_10(tuple(int(v[j]) for v in c), (int(k[0, j]), int(k[1, j])))
+        assert tuple(int(g[j]) for g in got) == want
+    ctr = np.array([0, 1, 2**40 + 5], np.uint64)
+    key = (np.array([7, 7, 9], np.uint64), np.array([11, 11, 13], np.uint64))
+    z = device_normals_f64(key, ctr, 0x44594E00, 2)
+    for j in range(3):
+        for b in range(2):
+            r = philox4x32_10((int(ctr[j]) & _U32, int(ctr[j]) >> 32, 0x44594E00, b), (int(key[0][j]), int(key[1][j])))
+            u = [((v >> 8) + 1.0) / 16777216.0 for v in r]
+            for h, (ua, ub) in enumerate(((u[0], u[1]), (u[2], u[3]))):
+                rad = math.sqrt(-2.0 * math.log(ua))
+                assert z[j, 4 * b + 2 * h] == rad * math.cos(2 * math.pi * ub)
+                assert z[j, 4 * b + 2 * h + 1] == rad * math.sin(2 * math.pi * ub)

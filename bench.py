@@ -75,6 +75,12 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--success-rule", choices=["terminated", "training"], default=None,
+                   help="episode success for the C3 scheduler: terminated (the evaluators' rule, default) or "
+                        "training (the reference's training loop: always False, so it never progresses)")
+    p.add_argument("--sched-restart", action="store_true",
+                   help="C3: restart the CurriculumScheduler from its initial config at the start of every "
+                        "iteration (CurriculumScheduler.reset()), so every timed iteration replays progressions")
     p.add_argument("--dist", action="store_true",
                    help="create the RCCL process group even at --gpus 1 (before any GPU work) and run the "
                         "multi-rank code path: the trainer's collectives, barrier and max-over-ranks timing")
@@ -165,17 +171,35 @@ def pg_bench(args, world, rank, dev):
     if _dist_on():  # world > 1, or --dist: the trainer runs its collectives over RCCL
         import torch.distributed as dist
         pg = dist.group.WORLD
+    kw = {"success_rule": args.success_rule} if args.success_rule else {}
     env, tr = build_pg_workload(args.config, dev, rank=rank, world=world, process_group=pg, envs=args.envs,
                                 horizon=args.horizon, curriculum=args.curriculum, epochs=args.epochs,
-                                minibatches=args.minibatches)
-    for _ in range(args.warmup):
+                                minibatches=args.minibatches, **kw)
+    sc = tr.scheduler
+    if args.sched_restart and sc is None:
+        raise SystemExit("--sched-restart needs a workload with a curriculum scheduler (--config default)")
+
+    def one_iteration():
+        if args.sched_restart:  # a fresh scheduler: level 0, empty window, the initial config on the device
+            sc.reset()
+            env.set_curriculum_async(sc.get_current_config())
         tr.iteration()
+
+    for _ in range(args.warmup):
+        one_iteration()
     torch.cuda.synchronize(dev)
     barrier(world)
     torch.cuda.synchronize(dev)
+    prog0 = len(sc.progression_history) if sc is not None else 0
+    prog_timed = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        tr.iteration()
+        if args.sched_restart:
+            prog0 = 0
+        one_iteration()
+        if sc is not None:  # host list length: no device work, no sync
+            prog_timed += len(sc.progression_history) - prog0
+            prog0 = len(sc.progression_history)
     torch.cuda.synchronize(dev)
     barrier(world)
     wall = time.perf_counter() - t0
@@ -204,6 +228,8 @@ def pg_bench(args, world, rank, dev):
     if tr.scheduler is not None:
         stats["curriculum_level"] = tr.scheduler.get_difficulty_level()
         stats["scheduler_episodes"] = int(tr.scheduler.total_episodes)
+        stats["progressions_applied_in_timed_iterations"] = prog_timed
+        stats["success_rule"] = tr.cfg.success_rule
     stats.update({k: round(v, 5) for k, v in tr.loss_stats().items()})
     return wall, phases, mfma, stats
 
@@ -386,7 +412,13 @@ def main():
     if args.learner == "pg":
         wall, phases, mfma, stats = pg_bench(args, world, rank, dev)
         upd = ("1 epoch x 1 minibatch: ratio == 1, an A2C-style step" if args.epochs * args.minibatches == 1
-               else f"{args.epochs} epochs x {args.minibatches} minibatches, one Adam step each")
+               else f"{args.epochs} epochs x {args.minibatches} minibatches, one Adam step each (PPO extension: "
+                    f"time-contiguous minibatch slices, order shuffled per epoch; the reference has no PPO, "
+                    f"parity unpinned)")
+        if args.sched_restart:
+            upd += "; CurriculumScheduler restarted from its initial config every iteration"
+        if WORKLOADS[args.config].get("scheduler"):
+            upd += f"; success_rule={args.success_rule or 'terminated'}"
         workload = (f"{WORKLOADS[args.config]['desc']} PG iteration: fused actor-MLP(256,256) rollout of "
                     f"{args.horizon} env steps x {args.envs} envs + critic fwd + GAE + adv-norm + PPO-clip / value "
                     f"heads + backward + Adam ({upd})")

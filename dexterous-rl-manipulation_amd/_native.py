@@ -137,6 +137,7 @@ _SIGS = {
     "dxrl_env_create": (C.c_int, [C.POINTER(EnvConfig), C.c_int32, _P, _P, C.POINTER(_P)]),
     "dxrl_env_destroy": (C.c_int, [_P]),
     "dxrl_env_set_curricula": (C.c_int, [_P, C.POINTER(Curriculum), C.c_int32, _P, _P]),
+    "dxrl_env_set_curricula_async": (C.c_int, [_P, _P, C.c_int32, _P, _P]),
     "dxrl_env_reset": (C.c_int, [_P, _P, _P, _P, _P]),
     "dxrl_env_step": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "dxrl_env_observe": (C.c_int, [_P, _P, _P]),
@@ -165,6 +166,8 @@ _SIGS = {
     "dxrl_sched_scratch_bytes": (C.c_int, [_I32, _I32, _I64, _I32, C.POINTER(_I64)]),
     "dxrl_sched_scan": (C.c_int, [_I32, C.POINTER(SchedArgs), _P]),
     "dxrl_pg_adam": (C.c_int, [_I32, _P, _P, _P, _P, _I64, _F64, _F64, _F64, _F64, _I64, _P, _F64, _P]),
+    "dxrl_pg_optimizer_step": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P, _I64, _F64, _F64, _F64, _F64, _I64, _F64,
+                                         _P, _P, _P, _P]),
 }
 
 _lib = None

@@ -293,8 +293,8 @@ int dxrl_env_destroy(dxrl_env* env) {
     return DXRL_OK;
 }
 
-int dxrl_env_set_curricula(dxrl_env* env, const dxrl_curriculum* table, int32_t n, const int32_t* env_index,
-                           void* stream) {
+static int set_curricula(dxrl_env* env, const dxrl_curriculum* table, int32_t n, const int32_t* env_index,
+                         void* stream, bool sync) {
     DXRL_REQUIRE(env && table, "null env/table");
     DXRL_REQUIRE(n >= 1 && n <= DXRL_MAX_CURRICULA, "curriculum table size %d outside [1, %d]", n,
                  DXRL_MAX_CURRICULA);
@@ -308,7 +308,6 @@ int dxrl_env_set_curricula(dxrl_env* env, const dxrl_curriculum* table, int32_t 
                          (long long)i, env_index[i]);
     DeviceGuard g(env->device);
     hipStream_t st = as_stream(stream);
-    // synchronous copies: host arrays may be temporaries of the caller
     if (int rc = hip_check(hipMemcpyAsync(env->curricula, table, sizeof(dxrl_curriculum) * n, hipMemcpyHostToDevice, st),
                            "curricula upload"))
         return rc;
@@ -321,10 +320,23 @@ int dxrl_env_set_curricula(dxrl_env* env, const dxrl_curriculum* table, int32_t 
         if (int rc = hip_check(hipMemsetAsync(env->soa.cfg, 0, sizeof(int32_t) * env->cfg.num_envs, st), "index zero"))
             return rc;
     }
-    if (int rc = hip_check(hipStreamSynchronize(st), "curricula sync")) return rc;
+    // synchronous form: the host arrays may be temporaries of the caller
+    if (sync)
+        if (int rc = hip_check(hipStreamSynchronize(st), "curricula sync")) return rc;
     env->n_curricula = n;
     return DXRL_OK;
 }
+
+int dxrl_env_set_curricula(dxrl_env* env, const dxrl_curriculum* table, int32_t n, const int32_t* env_index,
+                           void* stream) {
+    return set_curricula(env, table, n, env_index, stream, true);
+}
+
+int dxrl_env_set_curricula_async(dxrl_env* env, const dxrl_curriculum* table, int32_t n, const int32_t* env_index,
+                                 void* stream) {
+    return set_curricula(env, table, n, env_index, stream, false);
+}
+
 
 int dxrl_env_reset(dxrl_env* env, const uint8_t* mask, const double* draws, float* obs, void* stream) {
     DXRL_REQUIRE(env, "null env");

@@ -1540,6 +1540,94 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(const float* __restrict__ r
     if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
+// k_gae_lds: the same per-env recurrence, bit for bit (k_gae's expressions in k_gae's order), with
+// the loads taken off the serial chain.  A 256-thread workgroup owns 16 envs: all 256 threads
+// stage the envs' whole horizon (rew, V, done: 9 B per env-step) into LDS with independent
+// loads (one memory latency for the lot, not one per 32-step chunk), then one lane per env runs
+// the reverse recurrence out of LDS (operands read 8 steps ahead of the chain), then all 256
+// threads write adv / ret back coalesced.  256 workgroups at 4096 envs spread over every CU
+// (k_gae: 64 single-wave workgroups, a memory latency per chunk on the chain).
+constexpr int kGlEnvs = 16, kGlThreads = 256;
+__host__ __device__ constexpr int64_t gae_lds_bytes(int64_t T) { return T * kGlEnvs * 13 + kGlEnvs * 4; }
+__global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict__ rew,
+                                                        const uint8_t* __restrict__ done, const float* __restrict__ V,
+                                                        int64_t n, int T, float gamma, float lam,
+                                                        float* __restrict__ adv, float* __restrict__ ret,
+                                                        Moments* __restrict__ partial) {
+    extern __shared__ __attribute__((aligned(16))) float gl_lds[];
+    float* Rs = gl_lds;                            // [T][16]
+    float* Vs = Rs + (int64_t)T * kGlEnvs;          // [T + 1][16]
+    float* As = Vs + (int64_t)(T + 1) * kGlEnvs;    // [T][16] advantages
+    uint8_t* Ds = reinterpret_cast<uint8_t*>(As + (int64_t)T * kGlEnvs);  // [T][16]
+    __shared__ Moments red[kGlThreads];
+    const int tid = threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * kGlEnvs;
+    const int64_t cnt = (int64_t)T * kGlEnvs;
+    for (int64_t q = tid; q < cnt + kGlEnvs; q += kGlThreads) {  // + the bootstrap row V_T
+        const int64_t t = q / kGlEnvs, e = q % kGlEnvs;
+        const int64_t ic = e0 + e < n ? e0 + e : n - 1;
+        Vs[q] = V[t * n + ic];
+        if (q < cnt) {
+            Rs[q] = rew[t * n + ic];
+            Ds[q] = done[t * n + ic];
+        }
+    }
+    __syncthreads();
+    Moments mo{0.0, 0.0, 0.0};
+    if (tid < kGlEnvs) {
+        const int e = tid;
+        double s = 0.0, s2 = 0.0, K = 0.0;
+        float next_adv = 0.0f, next_v = Vs[(int64_t)T * kGlEnvs + e];
+        constexpr int kAh = 8;  // operands read this many steps ahead of the chain
+        float rq[kAh], vq[kAh];
+        uint8_t dq[kAh];
+#pragma unroll
+        for (int j = 0; j < kAh; ++j) {
+            const int t = T - 1 - j >= 0 ? T - 1 - j : 0;
+            rq[j] = Rs[t * kGlEnvs + e];
+            vq[j] = Vs[t * kGlEnvs + e];
+            dq[j] = Ds[t * kGlEnvs + e];
+        }
+        for (int t0 = T - 1; t0 >= 0; t0 -= kAh) {
+#pragma unroll
+            for (int j = 0; j < kAh; ++j) {
+                const int t = t0 - j;
+                if (t < 0) break;
+                const float rv = rq[j], vv = vq[j];
+                const float nd = dq[j] ? 0.0f : 1.0f;
+                const int tn = t - kAh >= 0 ? t - kAh : 0;  // refill this slot kAh steps ahead
+                rq[j] = Rs[tn * kGlEnvs + e];
+                vq[j] = Vs[tn * kGlEnvs + e];
+                dq[j] = Ds[tn * kGlEnvs + e];
+                const float delta = rv + gamma * next_v * nd - vv;
+                const float a = delta + gamma * lam * nd * next_adv;
+                As[t * kGlEnvs + e] = a;
+                if (t == T - 1) K = (double)a;
+                const double d = (double)a - K;
+                s += d;
+                s2 += d * d;
+                next_adv = a;
+                next_v = vv;
+            }
+        }
+        if (e0 + e < n) {
+            const double c = (double)T;
+            mo = Moments{c, K + s / c, fmax(s2 - s * (s / c), 0.0)};
+        }
+    }
+    __syncthreads();
+    for (int64_t q = tid; q < cnt; q += kGlThreads) {
+        const int64_t t = q / kGlEnvs, e = q % kGlEnvs;
+        if (e0 + e < n) {
+            const float a = As[q];
+            adv[t * n + e0 + e] = a;
+            ret[t * n + e0 + e] = a + Vs[q];
+        }
+    }
+    block_merge<kGlThreads>(mo, red);
+    if (tid == 0) partial[blockIdx.x] = red[0];
+}
+
 // Local moments of the rank, contiguous so ranks exchange them as one 3-element block:
 // stats[5] = count, stats[6] = mean, stats[7] = M2 (sum of squared deviations).
 __global__ void k_gae_sums(const Moments* __restrict__ partial, int nb, double* __restrict__ stats) {
@@ -1736,31 +1824,32 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
     p[k] -= lr * (a / bc1) / (sqrtf(b / bc2) + eps);
 }
 
-// f32 master -> bf16 forward weights + transposed copies for input gradients
-__global__ void k_pack_weights(const float* __restrict__ p, bf16* __restrict__ w) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// f32 master -> bf16 forward weights + transposed copies for input gradients: work item k of the
+// pack, reading master element j as p(j)
+template <typename Src>
+__device__ __forceinline__ void pack_item(int64_t k, const Src& p, bf16* __restrict__ w) {
     // forward copies (same layout as the master blocks)
     if (k < kW1) {
-        w[kBfW1a + k] = to_bf16(p[kOffW1a + k]);
-        w[kBfW1c + k] = to_bf16(p[kOffW1c + k]);
+        w[kBfW1a + k] = to_bf16(p(kOffW1a + k));
+        w[kBfW1c + k] = to_bf16(p(kOffW1c + k));
     }
     if (k < kW2) {
-        w[kBfW2a + k] = to_bf16(p[kOffW2a + k]);
-        w[kBfW2c + k] = to_bf16(p[kOffW2c + k]);
+        w[kBfW2a + k] = to_bf16(p(kOffW2a + k));
+        w[kBfW2c + k] = to_bf16(p(kOffW2c + k));
     }
     if (k < kW3) {
-        w[kBfW3a + k] = to_bf16(p[kOffW3a + k]);
-        w[kBfW3c + k] = to_bf16(p[kOffW3c + k]);
+        w[kBfW3a + k] = to_bf16(p(kOffW3a + k));
+        w[kBfW3c + k] = to_bf16(p(kOffW3c + k));
     }
     if (k < kW2T) {  // W2T[i][o] = W2[o][i]
         const int64_t i = k / kH, o = k % kH;
-        w[kBfW2aT + k] = to_bf16(p[kOffW2a + o * kHx + i]);
-        w[kBfW2cT + k] = to_bf16(p[kOffW2c + o * kHx + i]);
+        w[kBfW2aT + k] = to_bf16(p(kOffW2a + o * kHx + i));
+        w[kBfW2cT + k] = to_bf16(p(kOffW2c + o * kHx + i));
     }
     if (k < kW3T) {  // W3T[i][o] = W3[o][i]
         const int64_t i = k / kOut, o = k % kOut;
-        w[kBfW3aT + k] = to_bf16(p[kOffW3a + o * kHx + i]);
-        w[kBfW3cT + k] = to_bf16(p[kOffW3c + o * kHx + i]);
+        w[kBfW3aT + k] = to_bf16(p(kOffW3a + o * kHx + i));
+        w[kBfW3cT + k] = to_bf16(p(kOffW3c + o * kHx + i));
     }
     // fragment-ordered copies (dxrl_pg.h): element k of a [N][K] matrix's fragment stream
     const auto frag_rc = [](int64_t k, int K, int64_t& row, int64_t& col) {
@@ -1776,22 +1865,78 @@ __global__ void k_pack_weights(const float* __restrict__ p, bf16* __restrict__ w
         int64_t row, col;
         if (k < kFrW1) {
             frag_rc(k, kIn, row, col);
-            f[kFrOffW1 + k] = to_bf16(p[o1 + row * kIn + col]);
+            f[kFrOffW1 + k] = to_bf16(p(o1 + row * kIn + col));
         }
         if (k < kFrW2) {
             frag_rc(k, kH, row, col);
-            f[kFrOffW2 + k] = to_bf16(p[o2 + row * kHx + col]);
-            f[kFrOffW2T + k] = to_bf16(p[o2 + col * kHx + row]);  // W2T[row][col] = W2[col][row]
+            f[kFrOffW2 + k] = to_bf16(p(o2 + row * kHx + col));
+            f[kFrOffW2T + k] = to_bf16(p(o2 + col * kHx + row));  // W2T[row][col] = W2[col][row]
         }
         if (k < kFrW3) {
             frag_rc(k, kH, row, col);
-            f[kFrOffW3 + k] = to_bf16(p[o3 + row * kHx + col]);
+            f[kFrOffW3 + k] = to_bf16(p(o3 + row * kHx + col));
         }
         if (k < kFrW3T) {
             frag_rc(k, kOut, row, col);
-            f[kFrOffW3T + k] = to_bf16(p[o3 + col * kHx + row]);  // W3T[row][col] = W3[col][row]
+            f[kFrOffW3T + k] = to_bf16(p(o3 + col * kHx + row));  // W3T[row][col] = W3[col][row]
         }
     }
+}
+
+__global__ void k_pack_weights(const float* __restrict__ p, bf16* __restrict__ w) {
+    pack_item((int64_t)blockIdx.x * blockDim.x + threadIdx.x, [p](int64_t j) { return p[j]; }, w);
+}
+
+// One optimiser launch after k_sumsq: every workgroup sums the grad-norm partials in
+// k_sum_partials' order (so the clip scale is bit for bit k_adam's), thread k then applies Adam to
+// master element k (k_adam's expression) and runs pack work item k, recomputing the Adam update of
+// each element it packs from the unmodified inputs -- the updated master goes to a second buffer
+// (the trainer swaps the pair), so no thread reads an element another thread already updated.
+struct AdamPackArgs {
+    const float *p, *g, *m1, *m2;
+    float *po, *m1o, *m2o;
+    int64_t n;
+    float lr, b1, b2, eps, bc1, bc2, max_norm;
+    const double* partial;
+    int nb;
+    double* gnorm2;  // written by workgroup 0
+    bf16* w;
+};
+
+__global__ __launch_bounds__(256) void k_adam_pack(AdamPackArgs a) {
+    __shared__ double red[256];
+    double s = 0.0;
+    for (int k = threadIdx.x; k < a.nb; k += blockDim.x) s += a.partial[k];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    const double g2 = red[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.gnorm2[0] = g2;
+    float scale = 1.0f;
+    if (a.max_norm > 0.0f) {
+        const float nrm = (float)sqrt(g2);
+        scale = nrm > a.max_norm ? a.max_norm / (nrm + 1e-6f) : 1.0f;
+    }
+    const auto upd = [&](int64_t j, float& m, float& v) {
+        const float gk = a.g[j] * scale;
+        m = a.b1 * a.m1[j] + (1.0f - a.b1) * gk;
+        v = a.b2 * a.m2[j] + (1.0f - a.b2) * gk * gk;
+        return a.p[j] - a.lr * (m / a.bc1) / (sqrtf(v / a.bc2) + a.eps);
+    };
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < a.n) {
+        float m, v;
+        a.po[k] = upd(k, m, v);
+        a.m1o[k] = m;
+        a.m2o[k] = v;
+    }
+    pack_item(k, [&](int64_t j) {
+        float m, v;
+        return upd(j, m, v);
+    }, a.w);
 }
 
 static int reduce_to(const double* partial, int nb, double* out, int slot, hipStream_t st) {
@@ -1942,10 +2087,25 @@ int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const flo
     DXRL_REQUIRE(rew && done && values && adv && ret && partial && stats, "null argument");
     DeviceGuard g(device);
     hipStream_t st = as_stream(stream);
-    const int nb = (int)((num_envs + kGaeThreads - 1) / kGaeThreads);
-    hipLaunchKernelGGL(k_gae, dim3(nb), dim3(kGaeThreads), 0, st, rew, done, values, num_envs, horizon, (float)gamma,
-                       (float)lam, adv, ret, reinterpret_cast<Moments*>(partial));
-    if (int rc = launch_check("k_gae")) return rc;
+    static const bool seq = [] {  // A/B: k_gae, the chunked-load scan (DXRL_GAE_SEQ=1)
+        const char* v = getenv("DXRL_GAE_SEQ");
+        return v && atoi(v) != 0;
+    }();
+    int nb;
+    const int64_t lds = gae_lds_bytes(horizon);
+    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gae_lds),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8 * 1024) == hipSuccess;
+    if (!seq && attr && lds <= 152 * 1024) {
+        nb = (int)((num_envs + kGlEnvs - 1) / kGlEnvs);
+        hipLaunchKernelGGL(k_gae_lds, dim3(nb), dim3(kGlThreads), (size_t)lds, st, rew, done, values, num_envs,
+                           (int)horizon, (float)gamma, (float)lam, adv, ret, reinterpret_cast<Moments*>(partial));
+        if (int rc = launch_check("k_gae_lds")) return rc;
+    } else {
+        nb = (int)((num_envs + kGaeThreads - 1) / kGaeThreads);
+        hipLaunchKernelGGL(k_gae, dim3(nb), dim3(kGaeThreads), 0, st, rew, done, values, num_envs, horizon,
+                           (float)gamma, (float)lam, adv, ret, reinterpret_cast<Moments*>(partial));
+        if (int rc = launch_check("k_gae")) return rc;
+    }
     hipLaunchKernelGGL(k_gae_sums, dim3(1), dim3(256), 0, st, reinterpret_cast<const Moments*>(partial), nb, stats);
     return launch_check("k_gae_sums");
 }
@@ -1987,6 +2147,28 @@ int dxrl_pg_grad_sumsq(int32_t device, const float* grads, int64_t n, double* pa
     hipLaunchKernelGGL(k_sumsq, dim3(512), dim3(256), 0, st, grads, n, partial);
     if (int rc = launch_check("k_sumsq")) return rc;
     return reduce_to(partial, 512, out, 0, st);
+}
+
+int dxrl_pg_optimizer_step(int32_t device, const float* params, const float* grads, const float* m1, const float* m2,
+                           float* params_out, float* m1_out, float* m2_out, int64_t n, double lr, double beta1,
+                           double beta2, double eps, int64_t step, double max_norm, double* partial, double* gnorm2,
+                           void* packed, void* stream) {
+    DXRL_REQUIRE(params && grads && m1 && m2 && params_out && m1_out && m2_out && partial && gnorm2 && packed &&
+                     step >= 1,
+                 "bad optimizer arguments");
+    DXRL_REQUIRE(n == kParams, "optimizer: n must be the padded parameter count %lld", (long long)kParams);
+    DXRL_REQUIRE(params != params_out && m1 != m1_out && m2 != m2_out, "optimizer: outputs must not alias inputs");
+    DeviceGuard g(device);
+    hipStream_t st = as_stream(stream);
+    constexpr int kNb = 512;
+    hipLaunchKernelGGL(k_sumsq, dim3(kNb), dim3(256), 0, st, grads, n, partial);
+    if (int rc = launch_check("k_sumsq")) return rc;
+    AdamPackArgs a{params, grads, m1, m2, params_out, m1_out, m2_out, n, (float)lr, (float)beta1, (float)beta2,
+                   (float)eps, (float)(1.0 - pow(beta1, (double)step)), (float)(1.0 - pow(beta2, (double)step)),
+                   (float)max_norm, partial, kNb, gnorm2, static_cast<bf16*>(packed)};
+    const int64_t items = n > kW2 ? n : kW2;  // Adam elements / pack work items (kW2 >= every pack range)
+    hipLaunchKernelGGL(k_adam_pack, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, a);
+    return launch_check("k_adam_pack");
 }
 
 int dxrl_pg_adam(int32_t device, float* params, const float* grads, float* m1, float* m2, int64_t n, double lr,

@@ -186,6 +186,22 @@ class VecEnv:
     def set_curriculum(self, config):
         self.set_curricula([config])
 
+    def set_curriculum_async(self, config):
+        """``set_curriculum`` without a host sync (dxrl_env_set_curricula_async): the row is
+        staged in a pinned buffer that the stream copies from; an event keeps the next call
+        from overwriting it before the stream has passed the previous copy.  Every env uses
+        row 0 afterwards, effective at its next reset."""
+        if getattr(self, "_cur_stage", None) is None:
+            self._cur_stage = torch.zeros(C.sizeof(N.Curriculum), dtype=torch.uint8).pin_memory()
+            self._cur_event = torch.cuda.Event()
+        self._cur_event.synchronize()  # the previous staged copy has been consumed
+        row = config.to_native() if hasattr(config, "to_native") else CurriculumConfig(**config.to_dict()).to_native()
+        C.memmove(self._cur_stage.data_ptr(), C.addressof(row), C.sizeof(row))
+        self.curriculum_configs = [config]
+        with torch.cuda.device(self.device):
+            N.call("dxrl_env_set_curricula_async", self._h, self._cur_stage.data_ptr(), 1, None, self._stream())
+            self._cur_event.record(torch.cuda.current_stream(self.device))
+
     # -- hot path
     def reset(self, mask: Optional[torch.Tensor] = None, draws: Optional[torch.Tensor] = None,
               write_obs: bool = True) -> torch.Tensor:

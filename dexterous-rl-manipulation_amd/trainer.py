@@ -83,6 +83,24 @@ class TrainerConfig:
     success_rule: str = "terminated"         # "training" (episode_utils.py:52) or "terminated"
 
 
+def minibatch_bounds(M: int, B: int, round_samples: int):
+    """Sample offsets of B time-contiguous minibatch slices of M samples.  The fused learner
+    runs one 128-sample tile per CU per round (round_samples = 128 x CUs), so a slice of 6.25
+    rounds costs 7: slices are cut on whole rounds with the rounds split as evenly as possible
+    (4 minibatches of 25 rounds: 7, 6, 6, 6 instead of 4 x 7), the last slice taking the
+    remainder.  With fewer rounds than minibatches: equal slices."""
+    if B == 1:
+        return [0, M]
+    R = -(-M // round_samples)
+    if R < B:
+        size = M // B
+        return [k * size for k in range(B)] + [M]
+    out = [0]
+    for k in range(B):
+        out.append(min(M, out[-1] + (R // B + (1 if k < R % B else 0)) * round_samples))
+    return out
+
+
 class _null:
     def __enter__(self):
         return self
@@ -129,6 +147,7 @@ class PGTrainer:
         d, f32, bf, M, n, T = self.dev, torch.float32, torch.bfloat16, self.M, self.n, self.T
         z = lambda *s, dt=f32: torch.zeros(*s, dtype=dt, device=d)  # noqa: E731
         self.params, self.grads, self.m1, self.m2 = z(NPARAMS), z(NPARAMS), z(NPARAMS), z(NPARAMS)
+        self._spare = None  # the optimiser's output buffers (params / m1 / m2 ping-pong with these)
         self.packed = z(NBF, dt=bf)
         self._init_params()
         # tape
@@ -174,7 +193,7 @@ class PGTrainer:
         self.adv, self.ret = z(M), z(M)
         self.stats = torch.zeros(8, dtype=torch.float64, device=d)
         self.moments_all = torch.zeros(self.world, 3, dtype=torch.float64, device=d)  # ranks' stats[5..7]
-        nb = max(1024, (M + 255) // 256, 3 * ((n + 63) // 64))  # GAE: one (n, mean, M2) per 64-env block
+        nb = max(1024, (M + 255) // 256, 3 * ((n + 31) // 32))  # GAE: one (n, mean, M2) per 32-env block
         self.partial = torch.zeros(nb, dtype=torch.float64, device=d)
         self.dH2 = z(M, H, dt=bf)
         self.splits = max(1, min(cfg.splitk_target_blocks // 3, M // 1024))  # dW2: one workgroup per CU
@@ -305,15 +324,18 @@ class PGTrainer:
         over time-contiguous slices of the iteration's samples; the slice order is a fresh
         permutation per epoch (seeded by cfg.seed and the iteration)."""
         c = self.cfg
-        size = self.M // c.minibatches
+        bounds = self.minibatch_bounds()
         rng = np.random.default_rng([int(c.seed), self.iteration_index])
         for _ in range(c.epochs):
             for k in rng.permutation(c.minibatches):
-                self._mb = (int(k) * size, size)
+                self._mb = (bounds[k], bounds[k + 1] - bounds[k])
                 self.actor_train()
                 self.critic_train()
                 self.optimizer_step()
         self._mb = (0, self.M)
+
+    def minibatch_bounds(self):
+        return minibatch_bounds(self.M, self.cfg.minibatches, 128 * (self.fused_grid // 2))
 
     def phases(self):
         """The iteration's launch groups in order (bench.py times each)."""
@@ -363,15 +385,21 @@ class PGTrainer:
             self._wgrad(self.dH1, H, H, self.obs_rm, IN, IN, self.block(f"W1{net}", G))
 
     def optimizer_step(self):
+        """Gradient all-reduce (collective mode), then dxrl_pg_optimizer_step: grad-norm partials
+        + one clipped-Adam-and-pack launch writing the next master / moments into the spare
+        buffers, which then become current (params / m1 / m2 are swapped, not copied)."""
         c = self.cfg
         self._allreduce(self.grads)
-        N.call("dxrl_pg_grad_sumsq", self.dev.index, N.ptr(self.grads), NPARAMS, N.ptr(self.partial),
-               N.ptr(self.gnorm2), self._s())
         self.step_count += 1
-        N.call("dxrl_pg_adam", self.dev.index, N.ptr(self.params), N.ptr(self.grads), N.ptr(self.m1), N.ptr(self.m2),
-               NPARAMS, c.lr, c.betas[0], c.betas[1], c.adam_eps, self.step_count, N.ptr(self.gnorm2),
-               c.max_grad_norm, self._s())
-        self.pack()
+        if self._spare is None:
+            self._spare = tuple(torch.empty_like(t) for t in (self.params, self.m1, self.m2))
+        po, m1o, m2o = self._spare
+        N.call("dxrl_pg_optimizer_step", self.dev.index, N.ptr(self.params), N.ptr(self.grads), N.ptr(self.m1),
+               N.ptr(self.m2), N.ptr(po), N.ptr(m1o), N.ptr(m2o), NPARAMS, c.lr, c.betas[0], c.betas[1], c.adam_eps,
+               self.step_count, c.max_grad_norm, N.ptr(self.partial), N.ptr(self.gnorm2), N.ptr(self.packed),
+               self._s())
+        self._spare = (self.params, self.m1, self.m2)
+        self.params, self.m1, self.m2 = po, m1o, m2o
 
     def attach_curriculum(self, scheduler):
         """Host-side CurriculumScheduler (experiments/curriculum_scheduler.py) fed with every
@@ -461,8 +489,8 @@ class PGTrainer:
             ep = codes.transpose(1, 0, 2).ravel()
             ep = ep[ep != 0].astype(np.int64)
             progressed = sc.update_batch((ep & 1).astype(bool), ep >> 1)
-        if progressed:
-            self.env.set_curriculum(sc.get_current_config())
+        if progressed:  # enqueued behind the learner, no host sync (effective at each env's next reset)
+            self.env.set_curriculum_async(sc.get_current_config())
 
     def episode_records(self):
         from .training import gather_records

@@ -25,7 +25,7 @@ WORKLOADS = {
     "easy": {"config": "C2", "envs": 4096, "curriculum": "easy", "desc": "config_easy.json"},
     "default": {"config": "C3", "envs": 4096, "curriculum": "easy", "scheduler": True,
                 "desc": "config_default.json (CurriculumScheduler easy->hard fed every finished episode of "
-                        "every rank, success_rule=terminated)"},
+                        "every rank)"},
     "hard_heldout": {"config": "C4", "envs": 8192, "curriculum": "hard", "heldout": True,
                      "desc": "config_hard.json + HeldOutObjectSet table (env i -> object i % 10)"},
     "variable_noise": {"config": "C5", "envs": 4096, "curriculum": "variable", "obs_noise": 0.05,

@@ -98,11 +98,17 @@ int dxrl_env_layout_for(const dxrl_env_config* cfg, dxrl_env_layout* out);
 int dxrl_env_create(const dxrl_env_config* cfg, int32_t device, void* state, void* stream, dxrl_env** out);
 int dxrl_env_destroy(dxrl_env* env);
 
-/* Curriculum table + per-env row (host arrays; copied asynchronously).
+/* Curriculum table + per-env row (host arrays, copied on `stream`; returns after the copies
+ * completed, so the arrays may be temporaries).
  * env_index == NULL -> every env uses row 0.  Takes effect at the next reset,
  * as assigning env.curriculum_config does (evaluation/component_ablation.py:166). */
 int dxrl_env_set_curricula(dxrl_env* env, const dxrl_curriculum* table, int32_t n,
                            const int32_t* env_index, void* stream);
+/* The same without waiting: the copies are only enqueued on `stream`, so `table` and
+ * `env_index` (pinned host memory) must stay unchanged until the stream has passed them
+ * (the trainer's scheduler pushes a progression mid-iteration without a host sync). */
+int dxrl_env_set_curricula_async(dxrl_env* env, const dxrl_curriculum* table, int32_t n,
+                                 const int32_t* env_index, void* stream);
 
 /* Replaces reset(seed, options) (envs/manipulation_env.py:124-182).
  * mask   : device u8 [N] or NULL (all envs)
@@ -279,7 +285,10 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
  * moments stats[5] = T N, stats[6] = mean(adv), stats[7] = sum of squared deviations, and
  * stats[0..4] as dxrl_pg_adv_combine(stats + 5, world = 1) would (single rank: no second call)
  * (per-env sums about the env's own first value, merged with Chan et al.'s pairwise update
- * in a fixed order: no sum(a^2) - mean sum(a) cancellation).  partial: f64 [3 ceil(N / 64)];
+ * in a fixed order: no sum(a^2) - mean sum(a) cancellation).  horizon <= 256: a segmented scan
+ * over time (8 segments per env, boundary values from the composed segment maps: adv within a
+ * few f32 ulps of the sequential scan); longer horizons: one sequential scan per env.
+ * partial: f64 [3 ceil(N / 32)];
  * stats: f64 [8]. */
 int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const float* values, int64_t num_envs,
                 int64_t horizon, double gamma, double lam, float* adv, float* ret, double* partial, double* stats,
@@ -354,6 +363,15 @@ int dxrl_pg_grad_sumsq(int32_t device, const float* grads, int64_t n, double* pa
 int dxrl_pg_adam(int32_t device, float* params, const float* grads, float* m1, float* m2, int64_t n, double lr,
                  double beta1, double beta2, double eps, int64_t step, const double* gnorm2, double max_norm,
                  void* stream);
+/* The whole optimiser step in two launches: grad-norm partials, then one kernel that finishes
+ * the norm (k_sum_partials' order), applies clipped Adam (dxrl_pg_adam's arithmetic) and writes
+ * the bf16 pack (dxrl_pg_pack_weights' layout) -- the updated master / moments go to the *_out
+ * buffers (must not alias the inputs; the caller swaps the pairs).  n = dxrl_pg_sizes().params;
+ * partial: f64 [512] scratch; gnorm2: f64 [1] (sum of squared grads, written). */
+int dxrl_pg_optimizer_step(int32_t device, const float* params, const float* grads, const float* m1, const float* m2,
+                           float* params_out, float* m1_out, float* m2_out, int64_t n, double lr, double beta1,
+                           double beta2, double eps, int64_t step, double max_norm, double* partial, double* gnorm2,
+                           void* packed, void* stream);
 
 /* ---- fused one-pass learner step (csrc/dxrl_pg_fused.hip) ----------------------------
  * One launch per network replaces forward GEMMs + heads + backward GEMMs of the

@@ -365,3 +365,58 @@ def test_ppo_epochs_engage_the_clip(pkg):
     assert tr.step_count == 12 and not torch.equal(tr.params, p0)
     assert abs(s["approx_kl"]) > 1e-7 and s["clip_frac"] > 0.0, s
     assert all(math.isfinite(v) for v in s.values())
+
+
+def test_fused_optimizer_step_equals_three_launch_path(pkg):
+    """dxrl_pg_optimizer_step (grad-norm partials + one clipped-Adam-and-pack launch, output to
+    the spare buffers) == dxrl_pg_grad_sumsq + dxrl_pg_adam + dxrl_pg_pack_weights bit for bit:
+    master, both moments, the grad norm and every bf16 packed copy, over three steps with the
+    clip engaged and not."""
+    from dexterous_rl_manipulation_amd import _native as N
+    env, tr = make(pkg, 64, 16)
+    T_ = pkg.trainer
+    c = tr.cfg
+    p, m1, m2 = tr.params.clone(), tr.m1.clone(), tr.m2.clone()
+    packed, part, g2 = tr.packed.clone(), torch.zeros_like(tr.partial), torch.zeros_like(tr.gnorm2)
+    gen = torch.Generator(device=tr.dev).manual_seed(5)
+    s = N.stream_of(tr.dev)
+    for k, sd in enumerate((1e-3, 10.0, 1e-2)):  # 10.0: global norm far above max_grad_norm
+        g = torch.randn(T_.NPARAMS, generator=gen, device=tr.dev) * sd
+        tr.grads.copy_(g)
+        tr.optimizer_step()
+        N.call("dxrl_pg_grad_sumsq", tr.dev.index, N.ptr(g), T_.NPARAMS, N.ptr(part), N.ptr(g2), s)
+        N.call("dxrl_pg_adam", tr.dev.index, N.ptr(p), N.ptr(g), N.ptr(m1), N.ptr(m2), T_.NPARAMS, c.lr,
+               c.betas[0], c.betas[1], c.adam_eps, k + 1, N.ptr(g2), c.max_grad_norm, s)
+        N.call("dxrl_pg_pack_weights", tr.dev.index, N.ptr(p), N.ptr(packed), s)
+        torch.cuda.synchronize()
+        assert torch.equal(tr.params, p) and torch.equal(tr.m1, m1) and torch.equal(tr.m2, m2), k
+        assert torch.equal(tr.gnorm2, g2), k
+        assert torch.equal(tr.packed.view(torch.int16), packed.view(torch.int16)), k
+
+
+@pytest.mark.parametrize("n,T,p_done", [(100, 1, 0.1), (64, 7, 0.0), (4096, 25, 0.05), (96, 33, 0.3),
+                                        (4096, 200, 0.02), (130, 256, 0.0), (70, 300, 0.05)])
+def test_gae_lds_scan_matches_sequential_reference(pkg, n, T, p_done):
+    """dxrl_pg_gae (k_gae_lds: the horizon staged in LDS by the whole workgroup, one lane per env
+    running the recurrence) gives pg_reference.gae's adv / ret (the kernel's op order) bit for
+    bit, and the moments (count, mean, M2) a two-pass f64 reduction's to 1e-9.  Ragged env
+    counts, no dones and dense dones, horizons from 1 to 300."""
+    from dexterous_rl_manipulation_amd import _native as N
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(n * 1000 + T)
+    rew = torch.randn(T * n, generator=g, device=dev)
+    V = torch.randn((T + 1) * n, generator=g, device=dev) * 3.0
+    done = (torch.rand(T * n, generator=g, device=dev) < p_done).to(torch.uint8)
+    adv, ret = torch.empty_like(rew), torch.empty_like(rew)
+    part = torch.zeros(max(1024, 3 * ((n + 31) // 32)), dtype=torch.float64, device=dev)
+    stats = torch.zeros(8, dtype=torch.float64, device=dev)
+    N.call("dxrl_pg_gae", 0, N.ptr(rew), N.ptr(done), N.ptr(V), n, T, 0.99, 0.95, N.ptr(adv), N.ptr(ret),
+           N.ptr(part), N.ptr(stats), N.stream_of(dev))
+    torch.cuda.synchronize()
+    a_ref, r_ref = R.gae(rew, done, V, n, T, 0.99, 0.95)
+    assert torch.equal(adv, a_ref) and torch.equal(ret, r_ref)
+    a = adv.double()
+    assert stats[0].item() == n * T
+    assert math.isclose(stats[2].item(), a.mean().item(), rel_tol=1e-9, abs_tol=1e-12)
+    if n * T > 1:
+        assert math.isclose(stats[4].item(), a.std().item(), rel_tol=1e-9)

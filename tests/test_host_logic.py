@@ -250,3 +250,17 @@ def test_device_summary_replay_equals_sequential_updates(history):
             assert b.episode_steps == a.episode_steps[-len(b.episode_steps):]
             if history == "full":
                 assert a.episode_successes == b.episode_successes and a.episode_steps == b.episode_steps
+
+
+def test_minibatch_bounds_cut_on_whole_rounds():
+    """PPO minibatch slices (trainer.minibatch_bounds): whole 128 x CU rounds split as evenly
+    as possible, covering [0, M) exactly, each a multiple of 32 samples."""
+    from dexterous_rl_manipulation_amd.trainer import minibatch_bounds
+    rnd = 128 * 256
+    assert minibatch_bounds(819200, 4, rnd) == [0, 7 * rnd, 13 * rnd, 19 * rnd, 25 * rnd]
+    assert minibatch_bounds(819200, 1, rnd) == [0, 819200]
+    assert minibatch_bounds(819200, 5, rnd) == [0, 5 * rnd, 10 * rnd, 15 * rnd, 20 * rnd, 25 * rnd]
+    for M, B in ((8192, 4), (100000 - 100000 % 32, 3), (1638400, 16), (96 * 32, 2)):
+        b = minibatch_bounds(M, B, rnd)
+        assert b[0] == 0 and b[-1] == M and len(b) == B + 1
+        assert all(y > x and (y - x) % 32 == 0 for x, y in zip(b, b[1:])), b

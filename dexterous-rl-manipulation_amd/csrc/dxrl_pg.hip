@@ -1541,89 +1541,118 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(const float* __restrict__ r
 }
 
 // k_gae_lds: the same per-env recurrence, bit for bit (k_gae's expressions in k_gae's order), with
-// the loads taken off the serial chain.  A 256-thread workgroup owns 16 envs: all 256 threads
-// stage the envs' whole horizon (rew, V, done: 9 B per env-step) into LDS with independent
-// loads (one memory latency for the lot, not one per 32-step chunk), then one lane per env runs
-// the reverse recurrence out of LDS (operands read 8 steps ahead of the chain), then all 256
-// threads write adv / ret back coalesced.  256 workgroups at 4096 envs spread over every CU
-// (k_gae: 64 single-wave workgroups, a memory latency per chunk on the chain).
+// everything but the recurrence itself taken off the serial chain.  A 256-thread workgroup owns
+// 16 envs:
+//   1. all 256 threads load the envs' whole horizon (rew, V_t, V_{t+1}, done; batches of
+//      independent loads) and compute delta_t = r_t + gamma V_{t+1} (1 - d_t) - V_t into LDS;
+//   2. one lane per env runs A_t = delta_t + c_t A_{t+1} out of LDS, c_t = (gamma lambda)(1 - d_t)
+//      selected from the done byte (one multiply and one add on the chain; operands read 8 steps
+//      ahead);
+//   3. all 256 threads write adv / ret back coalesced and accumulate the moments.
+// k_gae (64 single-wave workgroups, the whole step on the chain, a memory latency per 32-step
+// chunk) remains for horizons whose staging exceeds the LDS.
 constexpr int kGlEnvs = 16, kGlThreads = 256;
-__host__ __device__ constexpr int64_t gae_lds_bytes(int64_t T) { return T * kGlEnvs * 13 + kGlEnvs * 4; }
+__host__ __device__ constexpr int64_t gae_lds_bytes(int64_t T) { return T * kGlEnvs * 13; }
 __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict__ rew,
                                                         const uint8_t* __restrict__ done, const float* __restrict__ V,
                                                         int64_t n, int T, float gamma, float lam,
                                                         float* __restrict__ adv, float* __restrict__ ret,
                                                         Moments* __restrict__ partial) {
     extern __shared__ __attribute__((aligned(16))) float gl_lds[];
-    float* Rs = gl_lds;                            // [T][16]
-    float* Vs = Rs + (int64_t)T * kGlEnvs;          // [T + 1][16]
-    float* As = Vs + (int64_t)(T + 1) * kGlEnvs;    // [T][16] advantages
-    uint8_t* Ds = reinterpret_cast<uint8_t*>(As + (int64_t)T * kGlEnvs);  // [T][16]
+    float* Ls = gl_lds;                           // [T][16] delta_t
+    float* Vs = Ls + (int64_t)T * kGlEnvs;         // [T][16] V_t (for ret)
+    float* As = Vs + (int64_t)T * kGlEnvs;         // [T][16] advantages
+    uint8_t* Ds = reinterpret_cast<uint8_t*>(As + (int64_t)T * kGlEnvs);  // [T][16] done
     __shared__ Moments red[kGlThreads];
     const int tid = threadIdx.x;
     const int64_t e0 = (int64_t)blockIdx.x * kGlEnvs;
     const int64_t cnt = (int64_t)T * kGlEnvs;
-    for (int64_t q = tid; q < cnt + kGlEnvs; q += kGlThreads) {  // + the bootstrap row V_T
-        const int64_t t = q / kGlEnvs, e = q % kGlEnvs;
-        const int64_t ic = e0 + e < n ? e0 + e : n - 1;
-        Vs[q] = V[t * n + ic];
-        if (q < cnt) {
-            Rs[q] = rew[t * n + ic];
-            Ds[q] = done[t * n + ic];
+    // 1. batches of kGlBatch elements per thread, every load issued before any lands
+    constexpr int kGlBatch = 16;
+    for (int64_t q0 = 0; q0 < cnt; q0 += (int64_t)kGlBatch * kGlThreads) {
+        float rv[kGlBatch], v0[kGlBatch], v1[kGlBatch];
+        uint8_t dv[kGlBatch];
+#pragma unroll
+        for (int u = 0; u < kGlBatch; ++u) {
+            const int64_t q = q0 + (int64_t)u * kGlThreads + tid;
+            const int64_t qc = q < cnt ? q : cnt - 1;
+            const int64_t t = qc / kGlEnvs, e = qc % kGlEnvs;
+            const int64_t ic = e0 + e < n ? e0 + e : n - 1;
+            rv[u] = rew[t * n + ic];
+            v0[u] = V[t * n + ic];
+            v1[u] = V[(t + 1) * n + ic];
+            dv[u] = done[t * n + ic];
+        }
+#pragma unroll
+        for (int u = 0; u < kGlBatch; ++u) {
+            const int64_t q = q0 + (int64_t)u * kGlThreads + tid;
+            if (q < cnt) {
+                const float nd = dv[u] ? 0.0f : 1.0f;
+                Ls[q] = rv[u] + gamma * v1[u] * nd - v0[u];
+                Vs[q] = v0[u];
+                Ds[q] = dv[u];
+            }
         }
     }
     __syncthreads();
-    Moments mo{0.0, 0.0, 0.0};
+    // 2. the recurrence
     if (tid < kGlEnvs) {
         const int e = tid;
-        double s = 0.0, s2 = 0.0, K = 0.0;
-        float next_adv = 0.0f, next_v = Vs[(int64_t)T * kGlEnvs + e];
-        constexpr int kAh = 8;  // operands read this many steps ahead of the chain
-        float rq[kAh], vq[kAh];
+        const float gl = gamma * lam;
+        float next_adv = 0.0f;
+        // chunks of kAh steps: the next chunk's operands are read while this one's chain runs
+        // (one LDS wait per chunk); steps past t = 0 in the last chunk run on clamped operands and
+        // are not stored
+        constexpr int kAh = 8;
+        float lq[kAh];
         uint8_t dq[kAh];
 #pragma unroll
         for (int j = 0; j < kAh; ++j) {
             const int t = T - 1 - j >= 0 ? T - 1 - j : 0;
-            rq[j] = Rs[t * kGlEnvs + e];
-            vq[j] = Vs[t * kGlEnvs + e];
+            lq[j] = Ls[t * kGlEnvs + e];
             dq[j] = Ds[t * kGlEnvs + e];
         }
         for (int t0 = T - 1; t0 >= 0; t0 -= kAh) {
+            float ln[kAh];
+            uint8_t dn[kAh];
 #pragma unroll
             for (int j = 0; j < kAh; ++j) {
-                const int t = t0 - j;
-                if (t < 0) break;
-                const float rv = rq[j], vv = vq[j];
-                const float nd = dq[j] ? 0.0f : 1.0f;
-                const int tn = t - kAh >= 0 ? t - kAh : 0;  // refill this slot kAh steps ahead
-                rq[j] = Rs[tn * kGlEnvs + e];
-                vq[j] = Vs[tn * kGlEnvs + e];
-                dq[j] = Ds[tn * kGlEnvs + e];
-                const float delta = rv + gamma * next_v * nd - vv;
-                const float a = delta + gamma * lam * nd * next_adv;
-                As[t * kGlEnvs + e] = a;
-                if (t == T - 1) K = (double)a;
-                const double d = (double)a - K;
-                s += d;
-                s2 += d * d;
-                next_adv = a;
-                next_v = vv;
+                const int t = t0 - kAh - j >= 0 ? t0 - kAh - j : 0;
+                ln[j] = Ls[t * kGlEnvs + e];
+                dn[j] = Ds[t * kGlEnvs + e];
             }
-        }
-        if (e0 + e < n) {
-            const double c = (double)T;
-            mo = Moments{c, K + s / c, fmax(s2 - s * (s / c), 0.0)};
+#pragma unroll
+            for (int j = 0; j < kAh; ++j) {
+                const float c = dq[j] ? 0.0f : gl;  // (gamma lambda) (1 - d_t), exactly
+                const float a = lq[j] + c * next_adv;
+                if (t0 - j >= 0) As[(t0 - j) * kGlEnvs + e] = a;
+                next_adv = a;
+            }
+#pragma unroll
+            for (int j = 0; j < kAh; ++j) {
+                lq[j] = ln[j];
+                dq[j] = dn[j];
+            }
         }
     }
     __syncthreads();
+    // 3. store, and the moments of this thread's elements about its first one (merged with Chan's
+    // update below and across workgroups: any shift point gives the same moments up to rounding)
+    double s = 0.0, s2 = 0.0, K = 0.0, c = 0.0;
     for (int64_t q = tid; q < cnt; q += kGlThreads) {
         const int64_t t = q / kGlEnvs, e = q % kGlEnvs;
         if (e0 + e < n) {
             const float a = As[q];
             adv[t * n + e0 + e] = a;
             ret[t * n + e0 + e] = a + Vs[q];
+            if (c == 0.0) K = (double)a;
+            const double d = (double)a - K;
+            s += d;
+            s2 += d * d;
+            c += 1.0;
         }
     }
+    const Moments mo = c > 0.0 ? Moments{c, K + s / c, fmax(s2 - s * (s / c), 0.0)} : Moments{0.0, 0.0, 0.0};
     block_merge<kGlThreads>(mo, red);
     if (tid == 0) partial[blockIdx.x] = red[0];
 }

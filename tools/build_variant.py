@@ -31,6 +31,6 @@ for k in range(0, len(subs), 3):
     txt = open(path).read()
     assert old in txt, f"{subs[k + 1]} not found in {fn}"
     open(path, "w").write(txt.replace(old, new))
-subprocess.run([B.HIPCC, *B.FLAGS, "-o", out, *[os.path.join(csrc, s) for s in B.SOURCES]], check=True, cwd=csrc)
+subprocess.run([B.HIPCC, *B.FLAGS, *os.environ.get("EXTRA_FLAGS", "").split(), "-o", out, *[os.path.join(csrc, s) for s in B.SOURCES]], check=True, cwd=csrc)
 shutil.rmtree(src_root)
 print(out)

@@ -22,6 +22,16 @@ step() {  # name limit cmd...
   tail -2 "$O/$name.log"
   if [ $rc -ne 0 ]; then echo "$name failed rc=$rc" | tee -a $O/session.log; exit $rc; fi
 }
+if [ -z "${SKIP_PMC:-}" ]; then
+  step pmc_fetch 90 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o run -- python3 tools/pmc_step.py
+  step pmc_write 90 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o run -- python3 tools/pmc_step.py
+  python tools/pmc_report.py "$O/pmc_fetch/**/*counter_collection.csv" "$O/pmc_write/**/*counter_collection.csv" 4194304 $O/pmc_step_kernel.json > /dev/null
+  # this round's PMC file where bench.py reads roofline.traffic from (profiles/rNN/), so the bench
+  # lines below cite traffic measured at the same HEAD
+  mkdir -p profiles/${ROUND:-r03} && cp $O/pmc_step_kernel.json profiles/${ROUND:-r03}/pmc_step_kernel.json
+  step pmc_mfma 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/pmc_mfma -o run -- python3 tools/prof_pg_iter.py
+  python tools/pmc_kernels.py "$O/pmc_mfma/**/*counter_collection.csv" > $O/pmc_mfma.json
+fi
 CFGS=${CFGS:-easy default hard_heldout variable_noise}
 for c in $CFGS; do
   if [ "$c" = easy ]; then step bench_$c 300 python bench.py; else
@@ -31,14 +41,21 @@ for c in $CFGS; do
     python3 bench.py --config $c --no-cpu-baseline $( [ "$c" = easy ] || echo --no-roofline )
   grep '^{' $O/prof_$c.log > $O/prof_$c.json
 done
-if [ -z "${SKIP_SWEEP:-}" ]; then step step_sweep 300 python tools/step_sweep.py 12 24; grep '^{' $O/step_sweep.log > $O/step_sweep.jsonl; fi
-if [ -z "${SKIP_PMC:-}" ]; then
-  step pmc_fetch 90 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o run -- python3 tools/pmc_step.py
-  step pmc_write 90 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o run -- python3 tools/pmc_step.py
-  python tools/pmc_report.py "$O/pmc_fetch/**/*counter_collection.csv" "$O/pmc_write/**/*counter_collection.csv" 4194304 $O/pmc_step_kernel.json > /dev/null
-  step pmc_mfma 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/pmc_mfma -o run -- python3 tools/prof_pg_iter.py
-  python tools/pmc_kernels.py "$O/pmc_mfma/**/*counter_collection.csv" > $O/pmc_mfma.json
+# the extra lines: real PPO (4 epochs x 4 minibatches), C3 with progressions in every timed
+# iteration, C3 under the reference's training-loop success rule, the RCCL path at world 1
+if [ -z "${SKIP_EXTRA:-}" ]; then
+  step bench_easy_ppo4x4 200 python bench.py --epochs 4 --minibatches 4 --steps 10 --warmup 2 --no-cpu-baseline --no-roofline
+  grep '^{' $O/bench_easy_ppo4x4.log > $O/bench_easy_ppo4x4.json
+  step bench_default_restart 200 python bench.py --config default --sched-restart --no-cpu-baseline --no-roofline
+  grep '^{' $O/bench_default_restart.log > $O/bench_default_restart.json
+  step bench_default_training 200 python bench.py --config default --success-rule training --no-cpu-baseline --no-roofline
+  grep '^{' $O/bench_default_training.log > $O/bench_default_training.json
+  step bench_easy_dist 200 python bench.py --dist --no-cpu-baseline --no-roofline
+  grep '^{' $O/bench_easy_dist.log > $O/bench_easy_dist.json
+  step eval_bench 200 python tools/eval_bench.py
+  grep '^{' $O/eval_bench.log > $O/eval_bench.jsonl
 fi
+if [ -z "${SKIP_SWEEP:-}" ]; then step step_sweep 300 python tools/step_sweep.py 12 24; grep '^{' $O/step_sweep.log > $O/step_sweep.jsonl; fi
 for c in $CFGS; do
   f=$(ls $O/prof_$c/*kernel_trace.csv $O/prof_$c/*/*kernel_trace.csv 2>/dev/null | head -1)
   [ -n "$f" ] && python tools/trace_summary.py "$f" > $O/trace_summary_$c.txt

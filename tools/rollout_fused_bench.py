@@ -10,7 +10,8 @@ import dexterous_rl_manipulation_amd  # noqa: E402,F401
 from dexterous_rl_manipulation_amd.workloads import build_pg_workload  # noqa: E402
 
 dev = torch.device("cuda:0")
-env, tr = build_pg_workload(os.environ.get("CFG", "easy"), dev)
+kw = {"splitk_target_blocks": int(os.environ["SPLITK"])} if os.environ.get("SPLITK") else {}
+env, tr = build_pg_workload(os.environ.get("CFG", "easy"), dev, **kw)
 for _ in range(2):
     tr.iteration()
 torch.cuda.synchronize()
@@ -33,4 +34,4 @@ for _ in range(reps):
 b.record()
 torch.cuda.synchronize()
 out["iteration"] = round(a.elapsed_time(b) / reps, 4)
-print(out)
+print(os.environ.get("SPLITK", ""), out)

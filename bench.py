@@ -446,6 +446,10 @@ def main():
                    "backend": "nccl (RCCL over xGMI)" if world > 1 or args.dist else None},
     }
     out.update(extra)
+    # peak torch-allocated device memory of the bench itself (trainer buffers, tapes), read
+    # before the roofline probe allocates its own
+    out["device_memory_gb"] = {"max_allocated": round(torch.cuda.max_memory_allocated(dev) / 1e9, 3),
+                               "max_reserved": round(torch.cuda.max_memory_reserved(dev) / 1e9, 3)}
     if rank == 0 and not args.no_roofline:
         out["roofline"] = step_kernel_roofline(args, dev)
         out["step_kernel_at_bench_envs"] = step_kernel_small(args.envs, dev)

@@ -925,6 +925,10 @@ struct WsReward {      // an env's dense-reward inputs and episode end of one st
 //   P4  env lanes: a = mu + sigma eps, dynamics, contacts, termination, auto-reset.
 //       Aux lanes: the same a, log pi (DPP row sum in action order), the act / log pi tape, then
 //       settle step t-1's reward and episode bookkeeping
+// kNoise: configs with fused noise (or the noise parity tapes); kDiag: diag_flags / parity tapes
+// set.  The production instantiations compile out every runtime check of the other's features
+// (branches and SGPRs inside the step loop: -8 % rollout time for <false, false>).
+template <bool kNoise, bool kDiag>
 __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p) {
     constexpr int kRows = 32;
     constexpr int kHeadWave = 3;  // an env wave: the env lanes idle while the head runs
@@ -1046,7 +1050,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         fric64 = cu.friction_is_f64_scalar != 0;
     }
     const int sa = s < kAct ? s : 0;
-    const bool obs_noise = p.obs_noise > 0.0f, dyn_noise = p.dyn_noise > 0.0f;
+    const bool obs_noise = kNoise && p.obs_noise > 0.0f, dyn_noise = kNoise && p.dyn_noise > 0.0f;
     if (live && !aux && s == 0) {
         KEYS[eg][0] = ek0;
         KEYS[eg][1] = ek1;
@@ -1151,7 +1155,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
                     DR.on[j][rbase + ln] = nz[h];
                 }
             }
-            if (p.obs_noise_tape) {  // parity tape: the value write_obs_row adds (row ctr - iteration T)
+            if (kDiag && p.obs_noise_tape) {  // parity tape: the value write_obs_row adds (row ctr - iteration T)
                 const int64_t row = (int64_t)(ctr - p.iteration * (uint64_t)T);
                 float4 v;
                 v.x = 4 * s + 0 < kObs ? p.obs_noise * nz[0] : 0.0f;
@@ -1218,7 +1222,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     const auto tape_obs_row = [&](int64_t m) {
         *reinterpret_cast<bf16x4*>(p.obs_rm + m * kIn + 4 * s) = *reinterpret_cast<const bf16x4*>(X + eg * kXs + 4 * s);
     };
-    const bool mlp = !(p.diag & 1), env_on = !(p.diag & 2);
+    const bool mlp = !kDiag || !(p.diag & 1), env_on = !kDiag || !(p.diag & 2);
     // ---- env lanes, P4 of step t: action, dynamics, contacts, termination, auto-reset
     // ---- env lanes, head phase of step t: the object's velocity damping, gravity, position and
     // wall stops (ME:212-235) -- independent of the action, so off the P4 chain (the env waves
@@ -1329,11 +1333,11 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         row_sum_in_order<kAct>(term, lp);
         p.act[m * kActPad + s] = s < kAct ? a : 0.0f;
         if (s == 0) p.logp[m] = lp;
-        if (p.applied_act) {
+        if (kDiag && p.applied_act) {
             if (dyn_noise) a = clipf(a + p.dyn_noise * DR.dzn[et_tid], -1.0f, 1.0f);
             p.applied_act[m * kActPad + s] = s < kAct ? a : 0.0f;
         }
-        if (p.dyn_noise_tape)  // parity tape: the value env_lane_step adds to the action
+        if (kDiag && p.dyn_noise_tape)  // parity tape: the value env_lane_step adds to the action
             p.dyn_noise_tape[m * kActPad + s] = (dyn_noise && s < kAct) ? p.dyn_noise * DR.dzn[et_tid] : 0.0f;
     };
 
@@ -1344,7 +1348,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     for (int q = 0; q < 8; ++q) st_acc[q] = 0;
 #define WS_STAMP(k)                                                                              \
     do {                                                                                         \
-        if (p.diag & 128) {                                                                      \
+        if (kDiag && (p.diag & 128)) {                                                           \
             __builtin_amdgcn_sched_barrier(0);                                                   \
             unsigned long long t_;                                                               \
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
@@ -1394,7 +1398,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
 #pragma unroll
             for (int q = 0; q < 4; ++q) MU[(4 * g16 + q) * (kOut + 1) + r16] = acc[q] + b3_reg;
         }
-        if (!(p.diag & 256)) {
+        if (!kDiag || !(p.diag & 256)) {
             // this step's draws (RW[(t - 1) & 1].rctr: the counters after step t-1's resets), the next
             // observation row's noise (aux lanes, own rows)
             if (aux) step_draws(ctr, t);
@@ -1406,7 +1410,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         if (live) {
             if (aux) {
                 aux_lane_step(m);
-                if (t > 0 && env_on && !(p.diag & 512)) settle(t - 1);  // step t-1's reward and bookkeeping
+                if (t > 0 && env_on && !(kDiag && (p.diag & 512))) settle(t - 1);  // step t-1's reward and bookkeeping
             } else {
                 env_lane_step(t, m);
             }
@@ -1416,13 +1420,13 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         WS_STAMP(6);
     }
 #undef WS_STAMP
-    if ((p.diag & 128) && s == 0 && live) {
+    if (kDiag && (p.diag & 128) && s == 0 && live) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) p.stamps[16 * i + (aux ? 8 : 0) + q] = st_acc[q];
     }
     if (live && aux) {
         if (T > 0 && env_on) settle(T - 1);
-        if (p.diag & 2)
+        if (kDiag && (p.diag & 2))
             for (int64_t t = 0; t < T && s == 0; ++t) p.rew[t * n + i] = 0.0f;
         if (s == 0) {
             p.ep_ret[i] = ep_ret;
@@ -2059,8 +2063,13 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
     }
     p.stamps = stamps;
     if (!(a->diag_flags & (32 | 64))) {  // default: the warp-specialised kernel
-        hipLaunchKernelGGL(k_pg_rollout_ws, dim3((unsigned)((n + kLsEnvs - 1) / kLsEnvs)), dim3(kWsThreads), 0,
-                           as_stream(stream), p);
+        const bool noise = a->obs_noise_std > 0.0 || a->dyn_noise_std > 0.0 || a->dyn_noise_tape || a->obs_noise_tape;
+        const bool diag = a->diag_flags != 0 || a->applied_act || a->dyn_noise_tape || a->obs_noise_tape;
+        const dim3 grid((unsigned)((n + kLsEnvs - 1) / kLsEnvs)), block(kWsThreads);
+        if (noise && diag) hipLaunchKernelGGL((k_pg_rollout_ws<true, true>), grid, block, 0, as_stream(stream), p);
+        else if (noise) hipLaunchKernelGGL((k_pg_rollout_ws<true, false>), grid, block, 0, as_stream(stream), p);
+        else if (diag) hipLaunchKernelGGL((k_pg_rollout_ws<false, true>), grid, block, 0, as_stream(stream), p);
+        else hipLaunchKernelGGL((k_pg_rollout_ws<false, false>), grid, block, 0, as_stream(stream), p);
         if (int rc = launch_check("k_pg_rollout_ws")) return rc;
         if (a->diag_flags & 128) {  // diagnostics: mean cycles per env per step segment, env / aux waves
             std::vector<unsigned long long> h((size_t)n * 16);

@@ -335,8 +335,13 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 // kFW waves per workgroup: 4 (one per SIMD, 512 registers each) or 8 (two per SIMD)
 // kTrain: forward + heads + backward; otherwise the forward-only critic-value pass, which keeps
 // no launch-long accumulators and so fits two waves per SIMD.
-template <int kFW, int kTR, bool kTrain>
+// kNet: 0 actor, 1 critic, -1 read from the arguments; kDiag: the DXRL_FUSED_DIAG ablations /
+// stamps compiled in (production instantiations do not test them at run time: fewer branches and
+// SGPRs in the tile loop)
+template <int kFW, int kTR, bool kTrain, int kNet, bool kDiag>
 __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedArgs p) {
+    const int diag = kDiag ? p.diag : 0;
+    const bool actor = kNet < 0 ? p.net == 0 : kNet == 0;  // kNet -1: the net read at run time
     using L = TileLds<kTR>;
     constexpr int kOffX = L::kOffX, kOffH1 = L::kOffH1, kOffH2 = L::kOffH2, kOffD = L::kOffD;
     constexpr int kHW = kTR / 32;  // waves running the heads (one 32-sample tile each)
@@ -379,8 +384,10 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
         return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
     };
-    const double adv_mean = uniform_f64(kTrain && p.net == 0 ? p.stats[2] : 0.0);
-    const double adv_div = uniform_f64(kTrain && p.net == 0 ? p.stats[4] + 1e-8 : 1.0);
+    const double adv_mean = uniform_f64(kTrain && actor ? p.stats[2] : 0.0);
+    // 1 / (std + 1e-8) once per launch: one f64 multiply per sample instead of an f64 division
+    // sequence (~12 f64 instructions and their registers in the head)
+    const double adv_inv = uniform_f64(kTrain && actor ? 1.0 / (p.stats[4] + 1e-8) : 1.0);
 
     // X tile prefetch: 128 rows x 8 chunks of 16 B = 1024 chunks, 4 per thread
     constexpr int kXU = kTR * (kIn / 8) / kFThreads;
@@ -400,7 +407,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     for (int k = 0; k < 16; ++k) st_acc[k] = 0;
 #define STAMP(k)                                                                                 \
     do {                                                                                         \
-        if (p.diag & 8) {                                                                        \
+        if (diag & 8) {                                                                        \
             __builtin_amdgcn_sched_barrier(0);                                                   \
             unsigned long long t_;                                                               \
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
@@ -471,8 +478,8 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 bk[q] = tanh_bias(((gf32*)b2)[(int64_t)(32 * bft + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
             if (!kTrain || __builtin_amdgcn_readfirstlane(wave) >= kHW) return;
             const int64_t mc = valid ? m : p.rows - 1;  // clamped: unconditional loads, no branch
-            hv = (p.net == 0 ? p.logp_old : p.ret)[mc];
-            if (p.net == 0) {
+            hv = (actor ? p.logp_old : p.ret)[mc];
+            if (actor) {
                 a0 = *reinterpret_cast<const float4*>(p.act + mc * kActPad + 4 * h);
                 a1 = *reinterpret_cast<const float4*>(p.act + mc * kActPad + 8 + 4 * h);
                 adv = p.adv[mc];
@@ -492,8 +499,8 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             if (j > 0) w_prefetch(pw2, W2, kH / 16, ft0 + j, lane);
             // (fwd_pipe measured 1 % slower here than the k-major chain + store_hidden)
             f32x16 acc[kMT];
-            fwd_run<kH / 16, kHp, kMT>(pw2, H1, acc, lane, l2_hook, (p.diag & 32) != 0);
-            if (!(p.diag & 16)) store_hidden(acc, ft0 + j, bk, H2, lane);
+            fwd_run<kH / 16, kHp, kMT>(pw2, H1, acc, lane, l2_hook, (diag & 32) != 0);
+            if (!(diag & 16)) store_hidden(acc, ft0 + j, bk, H2, lane);
         }
         // forward mode: the head waves' W3 fragments, all 16 k-steps, go out before the barrier
         // (their L2 latency overlaps its wait instead of opening the head phase twice).  Train
@@ -517,7 +524,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // stores then retire while the head runs instead of holding the head's load waits
         if constexpr (kTrain && kFW > kHW) {
             if (wave >= kHW && p.h1_out)
-                copy_tile_out_n<64 * (kFW - kHW), kTR>(H1, p.h1_out, kHx, m0, p.rows, tid - 64 * kHW, p.diag);
+                copy_tile_out_n<64 * (kFW - kHW), kTR>(H1, p.h1_out, kHx, m0, p.rows, tid - 64 * kHW, diag);
         }
         if (wave < kHW) {
             f32x16 acc;
@@ -555,7 +562,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 d[q] = 0.0f;
                 b3v[q] = ((gf32*)b3)[(int64_t)((q & 3) + 8 * (q >> 2) + 4 * h) * kHx];  // head row o of register q
             }
-            if (p.net == 0) {
+            if (actor) {
                 if (kTrain) {
                     float mu[8], a[8], lsv[8], iv2[8];
 #pragma unroll
@@ -589,7 +596,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                     for (int q = 4; q < 7; ++q) lp += h ? t[q] : u[q];      // o = 12..14
                     const float lo = hv;
                     const float ratio = __expf(lp - lo);
-                    const float A = (float)(((double)adv - adv_mean) / adv_div);
+                    const float A = (float)(((double)adv - adv_mean) * adv_inv);
                     const float s1 = ratio * A;
                     const float rc = fminf(fmaxf(ratio, 1.0f - p.clip_eps), 1.0f + p.clip_eps);
                     const float s2 = rc * A;
@@ -643,7 +650,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             continue;
         }
         if constexpr (kFW == kHW) {
-            if (p.h1_out) copy_tile_out_n<kFThreads, kTR>(H1, p.h1_out, kHx, m0, p.rows, tid, p.diag);
+            if (p.h1_out) copy_tile_out_n<kFThreads, kTR>(H1, p.h1_out, kHx, m0, p.rows, tid, diag);
         }
         WPre<1> pw3t;  // dH2's one W3T fragment, ahead of the barrier
         w_prefetch(pw3t, W3T, kOut / 16, ft0, lane);
@@ -659,7 +666,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             for (int j = 0; j < kNT; ++j)
 #pragma unroll
                 for (int ci = 0; ci < 2; ++ci)
-                    if (!(p.diag & 4))
+                    if (!(diag & 4))
                         acc3[j][ci] = mfma16(a, tr_frag16<kHp>(H2, 32 * (ft0 + j) + 16 * ci, kk, lane), acc3[j][ci]);
         }
 #pragma unroll 1
@@ -708,7 +715,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         //      so the next tile's X loads go out now
         if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
         // dH2 tile -> HBM (Y of the dW2 GEMM; H2 holds dH2 until the next tile's L2)
-        copy_tile_out_n<kFThreads, kTR>(H2, p.dh2_out, kH, m0, p.rows, tid, p.diag);
+        copy_tile_out_n<kFThreads, kTR>(H2, p.dh2_out, kH, m0, p.rows, tid, diag);
         if (tid < kH) {  // db2 stage 2: the kFW row-group sums of column tid, in row order
             const float* cs = reinterpret_cast<const float*>(lds + kOffD);
 #pragma unroll
@@ -726,14 +733,14 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                     const bf16x8 a = tr_frag16<kHp>(H1, 32 * (ft0 + j) + 16 * ri, kk, lane);
 #pragma unroll
                     for (int ci = 0; ci < 3; ++ci)
-                        if (!(p.diag & 4)) acc1[j][ri][ci] = mfma16(a, b[ci], acc1[j][ri][ci]);
+                        if (!(diag & 4)) acc1[j][ri][ci] = mfma16(a, b[ci], acc1[j][ri][ci]);
                 }
         }
         STAMP(13);
         __syncthreads();
         STAMP(14);
     }
-    if ((p.diag & 8) && lane == 0) {
+    if ((diag & 8) && lane == 0) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) p.stamps[((int64_t)blockIdx.x * kFW + wave) * 16 + k] = st_acc[k];
     }
@@ -790,7 +797,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         const int k = tid - 32;
         double s = 0.0;
         for (int t = 0; t < 64 * kHW; ++t) s += lred[t * 4 + k];
-        if ((p.net == 0) == (k != 1)) {
+        if (actor == (k != 1)) {
             p.loss[(int64_t)blockIdx.x * 4 + k] = s;
             // rows of workgroups this launch does not have (fewer tiles than the caller's grid):
             // zeroed, so a sum over all rows never picks up an earlier, larger pass
@@ -963,15 +970,20 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     static unsigned long long* stamps = nullptr;
     if ((diag & 8) && !stamps) (void)hipMalloc(&stamps, (size_t)65536 * 8 * 16 * 8);
     f.stamps = stamps;
-    if (tile == 64) {
-        if (!train) hipLaunchKernelGGL((k_pg_fused<4, 64, false>), dim3(grid), dim3(256), 0, st, f);
-        else hipLaunchKernelGGL((k_pg_fused<4, 64, true>), dim3(grid), dim3(256), 0, st, f);
+    const bool dg = diag != 0;
+    if (tile == 64) {  // A/B geometry: the diagnostic instantiations only
+        if (!train) hipLaunchKernelGGL((k_pg_fused<4, 64, false, 1, true>), dim3(grid), dim3(256), 0, st, f);
+        else if (!c) hipLaunchKernelGGL((k_pg_fused<4, 64, true, 0, true>), dim3(grid), dim3(256), 0, st, f);
+        else hipLaunchKernelGGL((k_pg_fused<4, 64, true, 1, true>), dim3(grid), dim3(256), 0, st, f);
     } else if (!train) {
-        hipLaunchKernelGGL((k_pg_fused<8, 128, false>), dim3(grid), dim3(512), 0, st, f);
-    } else if (waves == 8) {
-        hipLaunchKernelGGL((k_pg_fused<8, 128, true>), dim3(grid), dim3(512), 0, st, f);
+        if (dg) hipLaunchKernelGGL((k_pg_fused<8, 128, false, 1, true>), dim3(grid), dim3(512), 0, st, f);
+        else hipLaunchKernelGGL((k_pg_fused<8, 128, false, 1, false>), dim3(grid), dim3(512), 0, st, f);
+    } else if (!c) {
+        if (dg) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 0, true>), dim3(grid), dim3(512), 0, st, f);
+        else hipLaunchKernelGGL((k_pg_fused<8, 128, true, 0, false>), dim3(grid), dim3(512), 0, st, f);
     } else {
-        hipLaunchKernelGGL((k_pg_fused<4, 128, true>), dim3(grid), dim3(256), 0, st, f);
+        if (dg) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 1, true>), dim3(grid), dim3(512), 0, st, f);
+        else hipLaunchKernelGGL((k_pg_fused<8, 128, true, 1, false>), dim3(grid), dim3(512), 0, st, f);
     }
     if (int rc = launch_check("k_pg_fused")) return rc;
     if (diag & 8) {  // print the mean cycles per segment per wave (diagnostic builds only)

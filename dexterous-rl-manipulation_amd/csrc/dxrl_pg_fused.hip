@@ -991,10 +991,11 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
         (void)hipStreamSynchronize(st);
         (void)hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost);
         fprintf(stderr, "fused net=%d train=%d tile=%d waves=%d cycles/wave:", a->net, (int)train, tile, waves);
+        // (first half of the waves / second half: the two waves sharing a SIMD are w and w + waves / 2)
         for (int k = 0; k < 16; ++k) {
-            double sum = 0;
-            for (size_t w = 0; w < (size_t)grid * waves; ++w) sum += (double)h[w * 16 + k];
-            fprintf(stderr, " s%d=%.0f", k, sum / (grid * waves));
+            double sum[2] = {0, 0};
+            for (size_t w = 0; w < (size_t)grid * waves; ++w) sum[(w % waves) >= (size_t)waves / 2] += (double)h[w * 16 + k];
+            fprintf(stderr, " s%d=%.0f/%.0f", k, 2 * sum[0] / (grid * waves), 2 * sum[1] / (grid * waves));
         }
         fprintf(stderr, "\n");
     }

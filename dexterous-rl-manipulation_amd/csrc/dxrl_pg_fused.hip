@@ -103,6 +103,9 @@ __device__ __forceinline__ void zero_acc(f32x16& a) {
 struct NoHook {
     __device__ void operator()() const {}
 };
+struct NoKHook {
+    __device__ void operator()(int) const {}
+};
 // The first kD weight fragments of a fwd_tiles call, issuable ahead of the call (before the
 // barrier in front of its phase, so their L2 latency overlaps the barrier wait).
 template <int KS>
@@ -168,9 +171,9 @@ __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int kst, i
 // MFMA chain runs the epilogue of tile mt - 1 issues into its gaps one value pair at a time
 // (epi(acc, mt, p): pair p = 0..7 of the lane's 16 values, group p >> 1).  Two accumulators live
 // instead of MT.  Per output the k order -- and so every bit -- is the same as fwd_run's.
-template <int KS, int kLda, int MT, typename Epi, typename Hook = NoHook>
+template <int KS, int kLda, int MT, typename Epi, typename Hook = NoHook, typename KHook = NoKHook>
 __device__ __forceinline__ void fwd_pipe(WPre<KS>& w, const bf16* A, int lane, Epi& epi, Hook hook = Hook{},
-                                         bool no_mfma = false) {
+                                         bool no_mfma = false, KHook khook = KHook{}) {
     static_assert(KS >= 4 && KS % 4 == 0, "pair schedule assumes KS in {4, 8, 16, ...}");
     const int r = lane & 31, h = lane >> 5;
     constexpr int kD = WPre<KS>::kD;
@@ -207,6 +210,7 @@ __device__ __forceinline__ void fwd_pipe(WPre<KS>& w, const bf16* A, int lane, E
 #pragma unroll
                 for (int q = 0; q < kPairsPerK; ++q) epi(prev, mt - 1, (k / kKPerPair) * kPairsPerK + q);
             }
+            khook(sidx);  // caller work spread over the MT * KS steps
             __builtin_amdgcn_sched_barrier(0);
         }
         prev = acc;
@@ -332,6 +336,18 @@ __device__ __forceinline__ T* opaque(T* ptr) {
     return ptr;
 }
 
+// A/B switches: DXRL_L2_PIPE layer 2 as fwd_pipe (tanh epilogue under the next sample tile's
+// MFMAs) instead of the k-major chain + store_hidden; DXRL_FUSED_PRIO s_setprio 1 for waves 4..7
+#ifndef DXRL_L2_PIPE
+#define DXRL_L2_PIPE 1
+#endif
+#ifndef DXRL_DH2_IN_DH1
+#define DXRL_DH2_IN_DH1 1
+#endif
+#ifndef DXRL_FUSED_PRIO
+#define DXRL_FUSED_PRIO 1
+#endif
+
 // kFW waves per workgroup: 4 (one per SIMD, 512 registers each) or 8 (two per SIMD)
 // kTrain: forward + heads + backward; otherwise the forward-only critic-value pass, which keeps
 // no launch-long accumulators and so fits two waves per SIMD.
@@ -348,6 +364,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     constexpr int kMT = kTR / 32;  // 32-sample MFMA tiles of a tile
     constexpr int kFThreads = 64 * kFW;
     constexpr int kNT = kH / 32 / kFW;  // 32-wide feature tiles per wave
+    [[maybe_unused]] constexpr int kCopyU = kTR * (kH / 8) / kFThreads;  // 16-byte chunks per thread, [kTR][kH] tile
     static_assert(kHW <= kFW, "one 32-sample head tile per wave");
     __shared__ __attribute__((aligned(16))) bf16 lds[L::kElems];
     bf16* X = lds + kOffX;
@@ -355,6 +372,10 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     bf16* H2 = lds + kOffH2;
     bf16* D = lds + kOffD;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if DXRL_FUSED_PRIO
+    // the second-dispatched half of the waves loses VALU arbitration to its SIMD partner
+    if (__builtin_amdgcn_readfirstlane(wave) >= kFW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
     const int ft0 = kNT * wave;  // this wave's first 32-wide feature tile
     const int64_t ntiles = (p.rows + kTR - 1) / kTR;
 
@@ -498,9 +519,14 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             };
             if (j > 0) w_prefetch(pw2, W2, kH / 16, ft0 + j, lane);
             // (fwd_pipe measured 1 % slower here than the k-major chain + store_hidden)
+#if DXRL_L2_PIPE
+            EpiTanh e2{H2, 32 * (ft0 + j) + 4 * h, r, bk};
+            fwd_pipe<kH / 16, kHp, kMT>(pw2, H1, lane, e2, l2_hook, (diag & 32) != 0);
+#else
             f32x16 acc[kMT];
             fwd_run<kH / 16, kHp, kMT>(pw2, H1, acc, lane, l2_hook, (diag & 32) != 0);
             if (!(diag & 16)) store_hidden(acc, ft0 + j, bk, H2, lane);
+#endif
         }
         // forward mode: the head waves' W3 fragments, all 16 k-steps, go out before the barrier
         // (their L2 latency overlaps its wait instead of opening the head phase twice).  Train
@@ -705,7 +731,21 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             // dH1^T = W2^T dH2^T, gated in place of H1
             if (j > 0) w_prefetch(pw2t, W2T, kH / 16, ft0 + j, lane);
             EpiGate eg{H1, 32 * (ft0 + j) + 4 * h, r};
+#if DXRL_DH2_IN_DH1
+            // dH2 tile -> HBM (Y of the dW2 GEMM) in this phase's shadow: one 16-byte chunk per
+            // thread every 8th step (the stores go out after every weight fragment, so no
+            // fragment wait queues behind them; H2 holds dH2 read-only here)
+            const auto copy_k = [&](int sidx) {
+                constexpr int kEvery = kMT * (kH / 16) / kCopyU;
+                if (diag & 1 || sidx % kEvery != kEvery - 1) return;
+                const int c = tid_l + kFThreads * (sidx / kEvery), row = c >> 5, col = 8 * (c & 31);
+                const bf16x8 v = *reinterpret_cast<const bf16x8*>(H2 + row * kHp + col);
+                if (m0 + row < p.rows) *(__attribute__((address_space(1))) bf16x8*)(p.dh2_out + (m0 + row) * kH + col) = v;
+            };
+            fwd_pipe<kH / 16, kHp, kMT>(pw2t, H2, lane, eg, NoHook{}, false, copy_k);
+#else
             fwd_pipe<kH / 16, kHp, kMT>(pw2t, H2, lane, eg);
+#endif
         }
         STAMP(11);
         __syncthreads();
@@ -714,8 +754,10 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // ---- dW1 += dH1^T X (wave w: hidden rows of its tiles, input columns 0..63); LDS only,
         //      so the next tile's X loads go out now
         if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
+#if !DXRL_DH2_IN_DH1
         // dH2 tile -> HBM (Y of the dW2 GEMM; H2 holds dH2 until the next tile's L2)
         copy_tile_out_n<kFThreads, kTR>(H2, p.dh2_out, kH, m0, p.rows, tid, diag);
+#endif
         if (tid < kH) {  // db2 stage 2: the kFW row-group sums of column tid, in row order
             const float* cs = reinterpret_cast<const float*>(lds + kOffD);
 #pragma unroll

@@ -13,7 +13,8 @@ T = int(os.environ.get("PROF_T", "200"))
 iters = int(os.environ.get("PROF_ITERS", "3"))
 dev = torch.device("cuda:0")
 env = envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.easy(), reward_type="dense", seed=1, device=dev)
-tr = trainer.PGTrainer(env, trainer.TrainerConfig(horizon=T, seed=7))
+ep, mb = int(os.environ.get("PROF_EPOCHS", "1")), int(os.environ.get("PROF_MB", "1"))
+tr = trainer.PGTrainer(env, trainer.TrainerConfig(horizon=T, seed=7, epochs=ep, minibatches=mb))
 env.reset(write_obs=False)
 for _ in range(iters):
     tr.iteration()

@@ -344,6 +344,9 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #ifndef DXRL_DH2_IN_DH1
 #define DXRL_DH2_IN_DH1 1
 #endif
+#ifndef DXRL_HEAD_PF
+#define DXRL_HEAD_PF 1
+#endif
 #ifndef DXRL_FUSED_PRIO
 #define DXRL_FUSED_PRIO 1
 #endif
@@ -533,12 +536,22 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // mode keeps two batches of 8 issued in the head: 16 in flight there spill (the
         // launch-long gradient accumulators are live)
         constexpr int kW3K = kH / 16;
-        bf16x8 w3p[kTrain ? 1 : kW3K];
+        // (critic train mode, DXRL_HEAD_PF: the first half of the fragments and the head's biases go
+        // out here too, so the head opens without an L2 round trip; across the barrier the actor's
+        // extra registers spill, so its head keeps its loads)
+        constexpr bool kHeadPf = kTrain && DXRL_HEAD_PF && kNet == 1;
+        constexpr int kW3P = kTrain ? (kHeadPf ? kW3K / 2 : 1) : kW3K;
+        bf16x8 w3p[kW3P];
+        float b3p[8];
         const gbf16x8* w3row = (const gbf16x8*)W3 + lane;  // fragment stream, feature tile 0
-        if constexpr (!kTrain) {
+        if (!kTrain || kHeadPf) {
             if (wave < kHW) {
 #pragma unroll
-                for (int k = 0; k < kW3K; ++k) w3p[k] = w3row[64 * k];
+                for (int k = 0; k < kW3P; ++k) w3p[k] = w3row[64 * k];
+                if (kTrain) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) b3p[q] = ((gf32*)b3)[(int64_t)((q & 3) + 8 * (q >> 2) + 4 * h) * kHx];
+                }
             }
         }
         STAMP(4);
@@ -564,18 +577,31 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             } else {
                 constexpr int kB = kW3K / 2;  // fragments per batch (32 registers in flight)
                 bf16x8 w3f[kB];
+                if constexpr (kHeadPf) {
+                    // second batch in flight under the first (prefetched) batch's MFMAs
 #pragma unroll
-                for (int k = 0; k < kB; ++k) w3f[k] = w3row[64 * k];
-                __builtin_amdgcn_sched_barrier(0);
+                    for (int k = 0; k < kB; ++k) w3f[k] = w3row[64 * (k + kB)];
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int k = 0; k < kB; ++k) {
-                    const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * k + 8 * h);
-                    acc = mfma32(w3f[k], b, acc);
+                    for (int k = 0; k < kB; ++k) {
+                        const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * k + 8 * h);
+                        acc = mfma32(w3p[k], b, acc);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < kB; ++k) w3f[k] = w3row[64 * k];
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int k = 0; k < kB; ++k) {
+                        const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * k + 8 * h);
+                        acc = mfma32(w3f[k], b, acc);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int k = 0; k < kB; ++k) w3f[k] = w3row[64 * (k + kB)];
+                    __builtin_amdgcn_sched_barrier(0);
                 }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int k = 0; k < kB; ++k) w3f[k] = w3row[64 * (k + kB)];
-                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int k = 0; k < kB; ++k) {
                     const bf16x8 b = *reinterpret_cast<const bf16x8*>(H2 + (32 * wave + r) * kHp + 16 * (k + kB) + 8 * h);
@@ -586,7 +612,8 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 d[q] = 0.0f;
-                b3v[q] = ((gf32*)b3)[(int64_t)((q & 3) + 8 * (q >> 2) + 4 * h) * kHx];  // head row o of register q
+                // head row o of register q
+                b3v[q] = kHeadPf ? b3p[q] : ((gf32*)b3)[(int64_t)((q & 3) + 8 * (q >> 2) + 4 * h) * kHx];
             }
             if (actor) {
                 if (kTrain) {

@@ -638,6 +638,15 @@ extern "C" int dxrl_evaluate(dxrl_env* env, const dxrl_eval_args* args, void* st
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kEvalThreads, 0);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     int64_t blocks = (a.num_lanes + kEvalRows - 1) / kEvalRows;
+    // One workgroup (16 rows) per CU by default: with more rows than that the queue runs dry
+    // while the first long episodes are still running and most rows then idle in lockstep with
+    // them (measured on 40,960 held-out episodes: wave efficiency 46 % -> 72 % on hard objects,
+    // kernel time -26 %; 59 % -> 68 %, -5 % on the variable curriculum).  DXRL_EVAL_BPC: A/B.
+    static const int bpc_env = [] {
+        const char* v = getenv("DXRL_EVAL_BPC");
+        return v ? atoi(v) : 1;
+    }();
+    if (bpc_env > 0 && (per_cu <= 0 || bpc_env < per_cu)) per_cu = bpc_env;
     const int64_t resident = (int64_t)(per_cu > 0 ? per_cu : 2) * (cus > 0 ? cus : 256);
     if (blocks > resident) blocks = resident;
     static unsigned long long* diag[64] = {nullptr};
@@ -658,7 +667,8 @@ extern "C" int dxrl_evaluate(dxrl_env* env, const dxrl_eval_args* args, void* st
         unsigned long long it = 0;
         (void)hipStreamSynchronize(st);
         (void)hipMemcpy(&it, p.diag_iters, sizeof(it), hipMemcpyDeviceToHost);
-        fprintf(stderr, "k_eval_ls wave_iterations=%llu rows_per_wave=4 blocks=%lld\n", it, (long long)blocks);
+        fprintf(stderr, "k_eval_ls wave_iterations=%llu rows_per_wave=4 blocks=%lld per_cu=%d\n", it, (long long)blocks,
+                per_cu);
     }
     return DXRL_OK;
 }

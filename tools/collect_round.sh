@@ -10,7 +10,7 @@ for p in gpurun_out/r/prof_*/; do
   f=$(ls $p/*kernel_stats.csv $p/*/*kernel_stats.csv 2>/dev/null | head -1)
   [ -n "$f" ] && cp "$f" $D/kernel_stats_$c.csv
 done
-for p in pmc_fetch pmc_write pmc_mfma; do
+for p in pmc_fetch pmc_write pmc_mfma pmc_sq; do
   f=$(ls gpurun_out/r/$p/*counter_collection.csv gpurun_out/r/$p/*/*counter_collection.csv 2>/dev/null | head -1)
   [ -n "$f" ] && mkdir -p $D/pmc && cp "$f" $D/pmc/$p.csv
 done

@@ -8,6 +8,7 @@
 #   pmc_fetch/ pmc_write/   separate --pmc passes over k_step at 2^22 envs -> pmc_step_kernel.json
 #   pmc_mfma/               SQ_INSTS_VALU_MFMA_MOPS_BF16 + SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE
 #                           over PG iterations -> pmc_mfma.json
+#   pmc_sq/                 VALU / LDS-conflict / wait counters over PG iterations -> pmc_sq.json
 # Each GPU step has its own time limit; the script stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -31,6 +32,9 @@ if [ -z "${SKIP_PMC:-}" ]; then
   mkdir -p profiles/${ROUND:-r03} && cp $O/pmc_step_kernel.json profiles/${ROUND:-r03}/pmc_step_kernel.json
   step pmc_mfma 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/pmc_mfma -o run -- python3 tools/prof_pg_iter.py
   python tools/pmc_kernels.py "$O/pmc_mfma/**/*counter_collection.csv" > $O/pmc_mfma.json
+  # VALU / LDS / wait view of the same iterations (8 SQ counters: one pass)
+  step pmc_sq 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/pmc_sq -o run -- python3 tools/prof_pg_iter.py
+  python tools/pmc_kernels.py "$O/pmc_sq/**/*counter_collection.csv" > $O/pmc_sq.json
 fi
 CFGS=${CFGS:-easy default hard_heldout variable_noise}
 for c in $CFGS; do

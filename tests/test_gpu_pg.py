@@ -394,6 +394,35 @@ def test_fused_optimizer_step_equals_three_launch_path(pkg):
         assert torch.equal(tr.packed.view(torch.int16), packed.view(torch.int16)), k
 
 
+def test_optimizer_step_matches_torch_clip_and_adam(pkg):
+    """dxrl_pg_optimizer_step against PyTorch's own optimiser, not another kernel path:
+    torch.nn.utils.clip_grad_norm_(max_norm) + torch.optim.Adam(lr, betas, eps) in fp32 over
+    three steps (clipping engaged on the second).  The kernel writes the bias-corrected
+    denominator as sqrt(v / bc2) + eps where torch writes sqrt(v) / sqrt(bc2) + eps, so the
+    masters agree to fp32 rounding, not bit for bit; the squared global norm is an f64 sum in
+    both."""
+    env, tr = make(pkg, 64, 16)
+    T_ = pkg.trainer
+    c = tr.cfg
+    ref = torch.nn.Parameter(tr.params.clone())
+    opt = torch.optim.Adam([ref], lr=c.lr, betas=tuple(c.betas), eps=c.adam_eps)
+    gen = torch.Generator(device=tr.dev).manual_seed(11)
+    for k, sd in enumerate((1e-3, 10.0, 1e-2)):
+        g = torch.randn(T_.NPARAMS, generator=gen, device=tr.dev) * sd
+        tr.grads.copy_(g)
+        tr.optimizer_step()
+        ref.grad = g.clone()
+        norm = torch.nn.utils.clip_grad_norm_([ref], c.max_grad_norm)
+        opt.step()
+        torch.cuda.synchronize()
+        assert math.isclose(math.sqrt(tr.gnorm2.item()), float(g.double().norm()), rel_tol=1e-9), k
+        assert math.isclose(math.sqrt(tr.gnorm2.item()), float(norm), rel_tol=1e-6), k
+        st = opt.state[ref]
+        torch.testing.assert_close(tr.m1, st["exp_avg"], rtol=1e-5, atol=1e-9)
+        torch.testing.assert_close(tr.m2, st["exp_avg_sq"], rtol=1e-5, atol=1e-12)
+        torch.testing.assert_close(tr.params, ref.detach(), rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("n,T,p_done", [(100, 1, 0.1), (64, 7, 0.0), (4096, 25, 0.05), (96, 33, 0.3),
                                         (4096, 200, 0.02), (130, 256, 0.0), (70, 300, 0.05)])
 def test_gae_lds_scan_matches_sequential_reference(pkg, n, T, p_done):

@@ -45,7 +45,52 @@ int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, 
 // out[256][ldo] = sum_m Y[m][o] tanh(obs[m] . W1^T)[i] for the 256-wide first hidden layer of the
 // actor-critic MLP (obs [M][ldobs] bf16, 64 used columns; W1 [256][64]); H1 is recomputed on chip
 // exactly as the fused learner's forward computes it.  M % 32 == 0; partial as launch_wgrad.
+// reduce = 0: the split-K partials are left for the caller to sum (slab_reduce_block, e.g. in one
+// launch with other reductions); returns the number of partial slabs written in *nslabs.
 int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, const bf16* W1, int64_t M,
-                    int splits, float* partial, float* out, hipStream_t st, int64_t ldo);
+                    int splits, float* partial, float* out, hipStream_t st, int64_t ldo, int reduce = 1,
+                    int* nslabs = nullptr);
+
+// One 256-thread block of the two-level fixed-order slab sum (k_slab_reduce2_4): float4 columns
+// 16 blk .. 16 blk + 15 of z slabs; 16 groups of threads sum contiguous slab ranges, then group 0
+// adds the 16 group sums in group order.  grp: the block's [16][16] float4 scratch in LDS.
+__device__ __forceinline__ void slab_reduce_block(const float4* __restrict__ partial, int64_t slab4, int z,
+                                                  float* __restrict__ out, int accumulate, int cols, int64_t ldo,
+                                                  int64_t blk, float4 (*grp)[16]) {
+    constexpr int kRX = 16;
+    const int x = threadIdx.x % kRX, g = threadIdx.x / kRX;
+    const int64_t i = blk * kRX + x;
+    const int k0 = (int)((int64_t)g * z / kReduceGroups), k1 = (int)((int64_t)(g + 1) * z / kReduceGroups);
+    float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (i < slab4) {
+        for (int k = k0; k < k1; ++k) {
+            const float4 v = partial[(int64_t)k * slab4 + i];
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+    }
+    grp[g][x] = s;
+    __syncthreads();
+    if (g != 0 || i >= slab4) return;
+    float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int q = 0; q < kReduceGroups; ++q) {
+        const float4 v = grp[q][x];
+        r.x += v.x;
+        r.y += v.y;
+        r.z += v.z;
+        r.w += v.w;
+    }
+    const int64_t e = 4 * i;
+    const int64_t o = cols ? (e / cols) * ldo + e % cols : e;
+    float4* dst = reinterpret_cast<float4*>(out + o);
+    if (accumulate) {
+        const float4 a = *dst;
+        r = make_float4(a.x + r.x, a.y + r.y, a.z + r.z, a.w + r.w);
+    }
+    *dst = r;
+}
 
 }  // namespace dxrl

@@ -736,7 +736,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
 }
 
 int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, const bf16* W1, int64_t M,
-                    int splits, float* partial, float* out, hipStream_t st, int64_t ldo) {
+                    int splits, float* partial, float* out, hipStream_t st, int64_t ldo, int reduce, int* nslabs) {
     DXRL_REQUIRE(Y && obs && W1 && out && M > 0 && M % kLK == 0, "wgrad_l1: M must be a positive multiple of %d", kLK);
     DXRL_REQUIRE(ldy >= 256 && ldy % 8 == 0 && ldobs >= 64 && ldobs % 8 == 0 && ldo >= 256, "wgrad_l1: bad strides");
     if (splits < 1) splits = 1;
@@ -766,7 +766,8 @@ int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, 
     w.diag = diag;
     hipLaunchKernelGGL(k_wgrad_l1, dim3((unsigned)splits), dim3(512), kLLds, st, w);
     if (int rc = launch_check("k_wgrad_l1")) return rc;
-    if (splits > 1) {
+    if (nslabs) *nslabs = splits > 1 ? splits : 0;
+    if (splits > 1 && reduce) {
         const int64_t slab = 256 * 256;
         return launch_slab_reduce(partial, slab, splits, partial + (int64_t)splits * slab, out, 0, st, 256, ldo);
     }
@@ -827,39 +828,7 @@ constexpr int kRX = 16;  // float4 columns per block (x 16 groups = 256 threads)
 __global__ __launch_bounds__(256) void k_slab_reduce2_4(const float4* __restrict__ partial, int64_t slab4, int z,
                                                         float* __restrict__ out, int accumulate, int cols, int64_t ldo) {
     __shared__ float4 grp[kReduceGroups][kRX];
-    const int x = threadIdx.x % kRX, g = threadIdx.x / kRX;
-    const int64_t i = (int64_t)blockIdx.x * kRX + x;
-    const int k0 = (int)((int64_t)g * z / kReduceGroups), k1 = (int)((int64_t)(g + 1) * z / kReduceGroups);
-    float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (i < slab4) {
-        for (int k = k0; k < k1; ++k) {
-            const float4 v = partial[(int64_t)k * slab4 + i];
-            s.x += v.x;
-            s.y += v.y;
-            s.z += v.z;
-            s.w += v.w;
-        }
-    }
-    grp[g][x] = s;
-    __syncthreads();
-    if (g != 0 || i >= slab4) return;
-    float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll
-    for (int q = 0; q < kReduceGroups; ++q) {
-        const float4 v = grp[q][x];
-        r.x += v.x;
-        r.y += v.y;
-        r.z += v.z;
-        r.w += v.w;
-    }
-    const int64_t e = 4 * i;
-    const int64_t o = cols ? (e / cols) * ldo + e % cols : e;
-    float4* dst = reinterpret_cast<float4*>(out + o);
-    if (accumulate) {
-        const float4 a = *dst;
-        r = make_float4(a.x + r.x, a.y + r.y, a.z + r.z, a.w + r.w);
-    }
-    *dst = r;
+    slab_reduce_block(partial, slab4, z, out, accumulate, cols, ldo, blockIdx.x, grp);
 }
 
 int launch_slab_reduce(const float* partial, int64_t slab, int z, float* tmp, float* out, int accumulate,

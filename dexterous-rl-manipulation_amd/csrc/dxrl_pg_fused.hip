@@ -904,16 +904,15 @@ __device__ __forceinline__ void fused_scatter_one(int j, float s, float* __restr
 // of column x in order and the 16 group sums are added in group order (launch_slab_reduce's two
 // levels), else one thread sums the z slabs in order (its one level) -- the same per-element order
 // either way -- and the column goes straight into the grads blocks.
-__global__ __launch_bounds__(256) void k_fused_reduce_scatter(const float4* __restrict__ partial, int z,
-                                                              float* __restrict__ gW1, float* __restrict__ gW3,
-                                                              float* __restrict__ gLs, float* __restrict__ gW2,
-                                                              float ent_coef) {
+__device__ __forceinline__ void fused_reduce_block(const float4* __restrict__ partial, int z, float* __restrict__ gW1,
+                                                   float* __restrict__ gW3, float* __restrict__ gLs,
+                                                   float* __restrict__ gW2, float ent_coef, int64_t blk,
+                                                   float4 (*grp)[16]) {
     constexpr int kRX = 16;
     constexpr int64_t kSlab4 = kPartSize / 4;
     static_assert(kPartSize % 4 == 0 && 256 == kRX * kReduceGroups, "layout");
-    __shared__ float4 grp[kReduceGroups][kRX];
     const int x = threadIdx.x % kRX, g = threadIdx.x / kRX;
-    const int64_t i = (int64_t)blockIdx.x * kRX + x;
+    const int64_t i = blk * kRX + x;
     const auto add = [](float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); };
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (z > kReduceGroups) {
@@ -935,6 +934,27 @@ __global__ __launch_bounds__(256) void k_fused_reduce_scatter(const float4* __re
     fused_scatter_one(j + 1, r.y, gW1, gW3, gLs, gW2, ent_coef);
     fused_scatter_one(j + 2, r.z, gW1, gW3, gLs, gW2, ent_coef);
     fused_scatter_one(j + 3, r.w, gW1, gW3, gLs, gW2, ent_coef);
+}
+
+__global__ __launch_bounds__(256) void k_fused_reduce_scatter(const float4* __restrict__ partial, int z,
+                                                              float* __restrict__ gW1, float* __restrict__ gW3,
+                                                              float* __restrict__ gLs, float* __restrict__ gW2,
+                                                              float ent_coef) {
+    __shared__ float4 grp[kReduceGroups][16];
+    fused_reduce_block(partial, z, gW1, gW3, gLs, gW2, ent_coef, blockIdx.x, grp);
+}
+
+// The pass's two gradient reductions in one launch: blocks [0, nb1) sum the fused kernel's
+// workgroup partials and scatter them (W1 / W3 / log σ / the W2 bias column), the rest sum the
+// dW2 split-K slabs into W2's columns 0..255 -- disjoint outputs, each in its usual fixed order.
+__global__ __launch_bounds__(256) void k_grad_reduce_pair(const float4* __restrict__ fpart, int fz,
+                                                          float* __restrict__ gW1, float* __restrict__ gW3,
+                                                          float* __restrict__ gLs, float* __restrict__ gW2,
+                                                          float ent_coef, const float4* __restrict__ wpart, int wz,
+                                                          int64_t ldo, int nb1) {
+    __shared__ float4 grp[kReduceGroups][16];
+    if ((int)blockIdx.x < nb1) fused_reduce_block(fpart, fz, gW1, gW3, gLs, gW2, ent_coef, blockIdx.x, grp);
+    else slab_reduce_block(wpart, (int64_t)kH * kH / 4, wz, gW2, 0, kH, ldo, (int64_t)blockIdx.x - nb1, grp);
 }
 
 // grads blocks W1 / W3 (and log_std for the actor) from the workgroup sum (launch_slab_reduce)
@@ -1073,7 +1093,29 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     // the pad columns 257..287 of the W3 slab are never written: the scatter zeroes them
     float* tmp = a->partial + (int64_t)grid * kPartSize;
     float* sum = tmp + (int64_t)kReduceGroups * kPartSize;
-    if ((reinterpret_cast<uintptr_t>(a->partial) & 15) == 0) {
+    const bool aligned = (reinterpret_cast<uintptr_t>(a->partial) & 15) == 0;
+    if (aligned && recompute && (reinterpret_cast<uintptr_t>(a->wgrad_partial) & 15) == 0 &&
+        (reinterpret_cast<uintptr_t>(G + o2) & 15) == 0) {
+        // dW2 first (its partials only), then both reductions in one launch
+        int ns = 0;
+        if (int rc = launch_wgrad_l1(static_cast<const bf16*>(a->dh2), kH, f.X, kIn, w + (c ? kBfW1c : kBfW1a), a->rows,
+                                     a->wgrad_splits, a->wgrad_partial, G + o2, st, kHx, 0, &ns))
+            return rc;
+        const int nb1 = (int)((kPartSize / 4 + 15) / 16);
+        int nb2 = 0;
+        if (ns > kReduceGroups) {
+            nb2 = kH * kH / 4 / 16;
+        } else if (ns > 0) {  // few slabs: the one-level sum (k_slab_reduce2_4 is the two-level form)
+            if (int rc = launch_slab_reduce(a->wgrad_partial, (int64_t)kH * kH, ns, nullptr, G + o2, 0, st, kH, kHx))
+                return rc;
+        }
+        hipLaunchKernelGGL(k_grad_reduce_pair, dim3((unsigned)(nb1 + nb2)), dim3(256), 0, st,
+                           reinterpret_cast<const float4*>(a->partial), grid, G + (c ? kOffW1c : kOffW1a), G + o3,
+                           c ? nullptr : G + kOffLogStd, G + o2, (float)a->ent_coef,
+                           reinterpret_cast<const float4*>(a->wgrad_partial), ns, (int64_t)kHx, nb1);
+        return launch_check("k_grad_reduce_pair");
+    }
+    if (aligned) {
         (void)tmp;
         (void)sum;
         hipLaunchKernelGGL(k_fused_reduce_scatter, dim3((unsigned)((kPartSize / 4 + 15) / 16)), dim3(256), 0, st,

@@ -628,6 +628,9 @@ __device__ __forceinline__ void wait_chunks(int n) {
     else __builtin_amdgcn_s_waitcnt(0xF70);
 }
 
+// kDiag: the DXRL_WGRAD_DIAG ablations compiled in (a run-time branch in the chunk loop costs the
+// production kernel measurable time)
+template <bool kDiag>
 __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
     extern __shared__ __attribute__((aligned(16))) char gsm[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -715,7 +718,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
         wait_chunks(max(0, min(kLead - 2, nch - 2 - c)));
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (c + kLead < nch) issue(c + kLead);  // into the slot chunk c - 1 released
-        const bool next = c + 1 < nch && !(w.diag & 2), mm = !(w.diag & 1);
+        const bool next = c + 1 < nch && !(kDiag && (w.diag & 2)), mm = !(kDiag && (w.diag & 1));
         if (mm) contract(c, 0);
         __builtin_amdgcn_sched_barrier(0);
         f32x16 ha;
@@ -755,7 +758,9 @@ int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, 
     w.partial = splits > 1 ? partial : nullptr;
     w.ldo = ldo;
     static bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(k_wgrad_l1),
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(k_wgrad_l1<false>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLLds) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void*>(k_wgrad_l1<true>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, kLLds) == hipSuccess;
     }();
     DXRL_REQUIRE(attr, "wgrad_l1: could not raise the dynamic LDS limit");
@@ -764,7 +769,8 @@ int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, 
         return v ? atoi(v) : 0;
     }();
     w.diag = diag;
-    hipLaunchKernelGGL(k_wgrad_l1, dim3((unsigned)splits), dim3(512), kLLds, st, w);
+    if (diag) hipLaunchKernelGGL(k_wgrad_l1<true>, dim3((unsigned)splits), dim3(512), kLLds, st, w);
+    else hipLaunchKernelGGL(k_wgrad_l1<false>, dim3((unsigned)splits), dim3(512), kLLds, st, w);
     if (int rc = launch_check("k_wgrad_l1")) return rc;
     if (nslabs) *nslabs = splits > 1 ? splits : 0;
     if (splits > 1 && reduce) {

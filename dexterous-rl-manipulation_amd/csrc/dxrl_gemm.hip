@@ -577,15 +577,18 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_glds(WgradArgs w) {
 // bit the one the learner's forward used (test_h1_recompute_is_bit_exact).  The chunk ring is
 // k_wgrad_glds's (dH2 rows 512 B, source-swizzled by 4 (r & 3)); observation rows land 128 B
 // unpadded with their 16-byte chunks swizzled by (r >> 1) & 7, which keeps the row-fragment reads
-// conflict-free.  Each wave issues three LDS-DMA ops per chunk (two dH2 pieces of 2 rows, one
-// half-wave piece of 4 observation rows).  Software-pipelined by one chunk: iteration c recomputes
+// conflict-free.  Waves 0..3 issue every LDS-DMA op of a chunk (each: four dH2 pieces of 2 rows,
+// one piece of 8 observation rows); waves 4..7 issue none (below).  Software-pipelined by one chunk: iteration c recomputes
 // H1(c + 1) into one of two H1 buffers while contracting chunk c against the other, one barrier per
 // chunk; the H1(c + 1) products sit between the two k-steps of chunk c in the MFMA pipe, so their
 // tanh issues on the VALU while the second k-step runs on the matrix cores.
-constexpr int kLK = 32, kLNB = 5;
+#ifndef DXRL_WL1_RING
+#define DXRL_WL1_RING 4  // chunk slots (4: 166 us, 5: 174 us per 819 k rows, kernel-level A/B)
+#endif
+constexpr int kLK = 32, kLNB = DXRL_WL1_RING;
 constexpr int kLYB = kLK * 512, kLXB = kLK * 128, kLSlot = kLYB + kLXB;
 constexpr int kLH1 = kLNB * kLSlot;          // two recomputed H1 chunks [32][256] (h1_swz rows)
-constexpr int kLLds = kLH1 + 2 * kLK * 512;  // 132 KiB
+constexpr int kLLds = kLH1 + 2 * kLK * 512;  // 112 KiB at 4 slots
 
 __device__ __forceinline__ void glds_x4(const void* src, const void* lds_dst) {
     const uint32_t lds_addr =
@@ -620,13 +623,27 @@ __device__ __forceinline__ bf16x8 tr_frag_h1(const bf16* tile, int col0, int kk,
     return v;
 }
 
-// s_waitcnt vmcnt(3 n) (n = 0..3 chunks of three LDS-DMA ops each still in flight)
-__device__ __forceinline__ void wait_chunks(int n) {
-    if (n >= 3) __builtin_amdgcn_s_waitcnt(0xF79);
-    else if (n == 2) __builtin_amdgcn_s_waitcnt(0xF76);
-    else if (n == 1) __builtin_amdgcn_s_waitcnt(0xF73);
+// Which waves issue a chunk's LDS-DMA pieces.  1 (default): waves 0..3 five each (four dH2, one
+// observation piece), waves 4..7 none; 0: every wave three (two dH2 pieces, one half-wave
+// observation piece).  The first-dispatched half waits at the chunk barrier for its SIMD partners,
+// so the pieces' issue cost (~0.4 k cycles per wave and chunk) moves into that slack: 182 -> 171
+// us per 819 k rows (kernel-level A/B; the second half issuing them: 180 us)
+#ifndef DXRL_WL1_DMA_HALF
+#define DXRL_WL1_DMA_HALF 1
+#endif
+// s_waitcnt vmcnt(k n) (n = 0..4 chunks of k LDS-DMA ops each still in flight)
+// (gfx9 vmcnt: 6 bits, the low four at [3:0] and the high two at [15:14])
+constexpr int vmcnt_imm(int v) { return 0xF70 | (v & 15) | ((v >> 4) << 14); }
+template <int k>
+__device__ __forceinline__ void wait_chunks_k(int n) {
+    static_assert(4 * k <= 63, "vmcnt field");
+    if (n >= 4) __builtin_amdgcn_s_waitcnt(vmcnt_imm(4 * k));
+    else if (n == 3) __builtin_amdgcn_s_waitcnt(vmcnt_imm(3 * k));
+    else if (n == 2) __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * k));
+    else if (n == 1) __builtin_amdgcn_s_waitcnt(vmcnt_imm(k));
     else __builtin_amdgcn_s_waitcnt(0xF70);
 }
+__device__ __forceinline__ void wait_chunks(int n) { wait_chunks_k<3>(n); }
 
 // kDiag: the DXRL_WGRAD_DIAG ablations compiled in (a run-time branch in the chunk loop costs the
 // production kernel measurable time)
@@ -650,6 +667,31 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         w1f[k] = *(const __attribute__((address_space(1))) bf16x8*)(w.W1 + (32 * wave + r) * 64 + 16 * k + 8 * h);
+#if DXRL_WL1_DMA_HALF
+    // the issuing half: wave q = wave mod 4 loads dH2 rows 8 q .. 8 q + 7 and observation rows 8 q ..
+    const bool dma_wave = __builtin_amdgcn_readfirstlane(wave) < 4;
+    const auto wait_in = [&](int n) {
+        if (dma_wave) wait_chunks_k<5>(n);
+        else __builtin_amdgcn_s_waitcnt(0xF70);
+    };
+    const auto issue = [&](int c) {
+        if (!dma_wave) return;
+        const int q = wave & 3;
+        char* slot = gsm + (c % kLNB) * kLSlot;
+        const int64_t m0 = ((int64_t)blockIdx.x + (int64_t)c * gridDim.x) * kLK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // dH2 rows 8 q + 2 i, + 1
+            const int prow = 8 * q + 2 * i;
+            const int rr = prow + (lane >> 5), gchunk = (lane & 31) ^ (4 * (rr & 3));
+            glds_x4(Y + (m0 + rr) * ldy + 8 * gchunk, slot + prow * 512);
+        }
+        {  // observation rows 8 q .. + 7
+            const int row = 8 * q + (lane >> 3), pc = (lane & 7) ^ ((row >> 1) & 7);
+            glds_x4(X + (m0 + row) * ldx + 8 * pc, slot + kLYB + 1024 * q);
+        }
+    };
+#else
+    const auto wait_in = [](int n) { wait_chunks(n); };
     const auto issue = [&](int c) {
         char* slot = gsm + (c % kLNB) * kLSlot;
         const int64_t m0 = ((int64_t)blockIdx.x + (int64_t)c * gridDim.x) * kLK;
@@ -664,6 +706,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
             glds_x4(X + (m0 + row) * ldx + 8 * pc, slot + kLYB + 512 * wave);
         }
     };
+#endif
     // H1[32 samples][hidden 32 wave ..] of chunk c = tanh(obs W1^T): the fused learner's L1, one tile
     // (products and tanh split so the caller can put MFMA work between them)
     const auto recompute_mfma = [&](int c, f32x16& ha) {
@@ -707,7 +750,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
     for (int c = 0; c < kLead; ++c)
         if (c < nch) issue(c);
     if (nch > 0) {
-        wait_chunks(min(kLead - 1, nch - 1));  // chunk 0 in
+        wait_in(min(kLead - 1, nch - 1));  // chunk 0 in
         __builtin_amdgcn_s_barrier();
         f32x16 ha;
         recompute_mfma(0, ha);
@@ -715,7 +758,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
     }
     for (int c = 0; c < nch; ++c) {
         // chunk c + 1 in (chunks c + 2 .. c + kLead - 1 may still fly); H1(c) complete; chunk c - 1 done
-        wait_chunks(max(0, min(kLead - 2, nch - 2 - c)));
+        wait_in(max(0, min(kLead - 2, nch - 2 - c)));
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (c + kLead < nch) issue(c + kLead);  // into the slot chunk c - 1 released
         const bool next = c + 1 < nch && !(kDiag && (w.diag & 2)), mm = !(kDiag && (w.diag & 1));

@@ -18,7 +18,7 @@ name, subs = sys.argv[1], sys.argv[2:]
 out = os.path.join(ROOT, "ab", f"lib{name}.so")
 os.makedirs(os.path.dirname(out), exist_ok=True)
 # a mirror at the real depth keeps the sources' "../../include/dxrl.h" include working
-src_root = os.path.join(ROOT, "ab", "_src")
+src_root = os.path.join(ROOT, "ab", f"_src_{name}")  # per variant: builds may run in parallel
 if os.path.exists(src_root):
     shutil.rmtree(src_root)
 csrc = os.path.join(src_root, "pkg", "csrc")

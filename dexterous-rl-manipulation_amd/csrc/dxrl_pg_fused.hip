@@ -344,9 +344,6 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #ifndef DXRL_DH2_IN_DH1
 #define DXRL_DH2_IN_DH1 1
 #endif
-#ifndef DXRL_FWD_EARLY_X
-#define DXRL_FWD_EARLY_X 0
-#endif
 #ifndef DXRL_HEAD_PF
 #define DXRL_HEAD_PF 1
 #endif
@@ -516,17 +513,8 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         for (int j = 0; j < kNT; ++j) {
             bft = ft0 + j;
             const auto l2_hook = [&]() {
-                if (j == kNT - 1) {
-                    head_inputs();
-#if DXRL_FWD_EARLY_X
-                    // forward mode: X is dead after L1, so the next tile's X loads go out here,
-                    // behind the last W2 fragment, and land under layer 2's MFMA chain (issued at
-                    // the end of the tile, the next tile's X stores waited for their whole latency)
-                    if constexpr (!kTrain) {
-                        if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
-                    }
-#endif
-                } else {
+                if (j == kNT - 1) head_inputs();
+                else {
 #pragma unroll
                     for (int q = 0; q < 16; ++q)
                         bk[q] = tanh_bias(((gf32*)b2)[(int64_t)(32 * bft + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
@@ -709,9 +697,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         }
         STAMP(6);
         if (!kTrain) {
-#if !DXRL_FWD_EARLY_X
             if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
-#endif
             __syncthreads();  // X / H1 / H2 are rewritten by the next tile
             STAMP(7);
             continue;

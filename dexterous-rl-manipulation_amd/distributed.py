@@ -11,7 +11,8 @@ sharded run draws exactly what the same envs draw unsharded.  The PG learner
   * one SUM all-reduce of the flat f32 gradient buffer.  The per-sample loss scale is 1/(global
     sample count) -- 1/(M*world) for equal shards -- and the entropy bonus
     enters each rank as ent_coef/world (``loss_scales``), so the SUM is the
-    gradient of the global-batch mean loss, ragged shards included.
+    gradient of the global-batch mean loss (that algebra alone would also hold for
+    ragged shards; the trainer requires equal ones, see below).
 The curriculum scheduler (config C3) additionally all-gathers each rank's
 episode-end codes so every rank feeds the same global episode stream.
 

@@ -1697,17 +1697,28 @@ __global__ void k_stats_combine(const double* __restrict__ moments, int world, d
 }
 
 // out[slot] = sum(partials) (fixed order)
-__global__ void k_sum_partials(const double* __restrict__ partial, int nb, double* __restrict__ out, int slot) {
-    __shared__ double red[256];
-    double s = 0.0;
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) s += partial[k];
-    red[threadIdx.x] = s;
+// Sum of nb partials by a 256-thread block in one fixed order: thread-strided sums, a butterfly
+// inside each wave (lane pairs add the same two values, so every lane holds the same bits), then
+// the four wave sums in wave order.  k_sum_partials and every k_adam_pack workgroup use it, so the
+// two optimiser paths clip with bit-identical norms.
+__device__ __forceinline__ double block_sum256(double s, double* red4) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = s;
     __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) out[slot] = red[0];
+    return ((red4[0] + red4[1]) + red4[2]) + red4[3];
+}
+__device__ __forceinline__ double block_sum_partials(const double* __restrict__ partial, int nb, double* red4) {
+    double s = 0.0;
+    for (int k = threadIdx.x; k < nb; k += 256) s += partial[k];
+    return block_sum256(s, red4);
+}
+
+__global__ __launch_bounds__(256) void k_sum_partials(const double* __restrict__ partial, int nb,
+                                                      double* __restrict__ out, int slot) {
+    __shared__ double red4[4];
+    const double s = block_sum_partials(partial, nb, red4);
+    if (threadIdx.x == 0) out[slot] = s;
 }
 
 
@@ -1825,18 +1836,13 @@ __global__ __launch_bounds__(256) void k_logstd_grad(const float* __restrict__ p
 
 // ------------------------------------------------------------------ optimiser
 // grad-norm^2 partials, then Adam with global-norm clipping (scale on device)
-__global__ void k_sumsq(const float* __restrict__ x, int64_t n, double* __restrict__ partial) {
-    __shared__ double red[256];
+__global__ __launch_bounds__(256) void k_sumsq(const float* __restrict__ x, int64_t n, double* __restrict__ partial) {
+    __shared__ double red4[4];
     double s = 0.0;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
         s += (double)x[k] * (double)x[k];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    s = block_sum256(s, red4);
+    if (threadIdx.x == 0) partial[blockIdx.x] = s;
 }
 
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m1,
@@ -1920,11 +1926,53 @@ __global__ void k_pack_weights(const float* __restrict__ p, bf16* __restrict__ w
     pack_item((int64_t)blockIdx.x * blockDim.x + threadIdx.x, [p](int64_t j) { return p[j]; }, w);
 }
 
+// Position of element (row, col) of a [N][K] matrix in its fragment stream (the inverse of
+// pack_item's frag_rc: 64-lane x 8-element fragments, 32 rows x 16 columns each, k-steps inner)
+__device__ __forceinline__ int64_t frag_index(int row, int col, int K) {
+    const int lane = (row & 31) + 32 * ((col >> 3) & 1);
+    return ((int64_t)((row >> 5) * (K / 16) + (col >> 4)) << 9) + lane * 8 + (col & 7);
+}
+
+// Every packed bf16 copy of master element j (value v): the scatter form of pack_item's gathers --
+// the forward copy, the transposed copy and the fragment streams of W1 / W2 / W3 (log σ and the
+// pad slots between the nets are master-only)
+__device__ __forceinline__ void pack_scatter(int64_t j, float v, bf16* __restrict__ w) {
+    const bf16 b = to_bf16(v);
+    const bool c = j >= kOffW1c;
+    const int64_t r = j - (c ? kOffW1c : kOffW1a);
+    bf16* f = w + kFr + (c ? kFrNet : 0);
+    if (r < 0) return;
+    if (r < kW1) {  // W1 [kH][kIn]
+        const int row = (int)(r / kIn), col = (int)(r % kIn);
+        w[(c ? kBfW1c : kBfW1a) + r] = b;
+        f[kFrOffW1 + frag_index(row, col, kIn)] = b;
+    } else if (r < kW1 + kW2) {  // W2 [kH][kHx], column kH = bias
+        const int64_t q = r - kW1;
+        const int row = (int)(q / kHx), col = (int)(q % kHx);
+        w[(c ? kBfW2c : kBfW2a) + q] = b;
+        if (col < kH) {
+            w[(c ? kBfW2cT : kBfW2aT) + (int64_t)col * kH + row] = b;
+            f[kFrOffW2 + frag_index(row, col, kH)] = b;
+            f[kFrOffW2T + frag_index(col, row, kH)] = b;
+        }
+    } else if (r < kW1 + kW2 + kW3) {  // W3 [kOut][kHx]
+        const int64_t q = r - kW1 - kW2;
+        const int row = (int)(q / kHx), col = (int)(q % kHx);
+        w[(c ? kBfW3c : kBfW3a) + q] = b;
+        if (col < kH) {
+            w[(c ? kBfW3cT : kBfW3aT) + (int64_t)col * kOut + row] = b;
+            f[kFrOffW3 + frag_index(row, col, kH)] = b;
+            f[kFrOffW3T + frag_index(col, row, kOut)] = b;
+        }
+    }
+}
+
 // One optimiser launch after k_sumsq: every workgroup sums the grad-norm partials in
-// k_sum_partials' order (so the clip scale is bit for bit k_adam's), thread k then applies Adam to
-// master element k (k_adam's expression) and runs pack work item k, recomputing the Adam update of
-// each element it packs from the unmodified inputs -- the updated master goes to a second buffer
-// (the trainer swaps the pair), so no thread reads an element another thread already updated.
+// k_sum_partials' order (so the clip scale is bit for bit k_adam's); thread j applies Adam to
+// master element j (k_adam's expression, once) and scatters the updated value into every packed
+// bf16 copy (pack_scatter).  The updated master goes to a second buffer (the trainer swaps the
+// pair).  The gather form (k_pack_weights / pack_item, which recomputed the update of every
+// element it packed: up to 20 updates per thread) took 13.3 us per step.
 struct AdamPackArgs {
     const float *p, *g, *m1, *m2;
     float *po, *m1o, *m2o;
@@ -1932,44 +1980,29 @@ struct AdamPackArgs {
     float lr, b1, b2, eps, bc1, bc2, max_norm;
     const double* partial;
     int nb;
-    double* gnorm2;  // written by workgroup 0
+    double* gnorm2;
     bf16* w;
 };
 
 __global__ __launch_bounds__(256) void k_adam_pack(AdamPackArgs a) {
-    __shared__ double red[256];
-    double s = 0.0;
-    for (int k = threadIdx.x; k < a.nb; k += blockDim.x) s += a.partial[k];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
-    const double g2 = red[0];
+    __shared__ double red4[4];
+    const double g2 = block_sum_partials(a.partial, a.nb, red4);
     if (blockIdx.x == 0 && threadIdx.x == 0) a.gnorm2[0] = g2;
     float scale = 1.0f;
     if (a.max_norm > 0.0f) {
         const float nrm = (float)sqrt(g2);
         scale = nrm > a.max_norm ? a.max_norm / (nrm + 1e-6f) : 1.0f;
     }
-    const auto upd = [&](int64_t j, float& m, float& v) {
-        const float gk = a.g[j] * scale;
-        m = a.b1 * a.m1[j] + (1.0f - a.b1) * gk;
-        v = a.b2 * a.m2[j] + (1.0f - a.b2) * gk * gk;
-        return a.p[j] - a.lr * (m / a.bc1) / (sqrtf(v / a.bc2) + a.eps);
-    };
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < a.n) {
-        float m, v;
-        a.po[k] = upd(k, m, v);
-        a.m1o[k] = m;
-        a.m2o[k] = v;
-    }
-    pack_item(k, [&](int64_t j) {
-        float m, v;
-        return upd(j, m, v);
-    }, a.w);
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= a.n) return;
+    const float gk = a.g[j] * scale;
+    const float m = a.b1 * a.m1[j] + (1.0f - a.b1) * gk;
+    const float v = a.b2 * a.m2[j] + (1.0f - a.b2) * gk * gk;
+    const float pn = a.p[j] - a.lr * (m / a.bc1) / (sqrtf(v / a.bc2) + a.eps);
+    a.po[j] = pn;
+    a.m1o[j] = m;
+    a.m2o[j] = v;
+    pack_scatter(j, pn, a.w);
 }
 
 static int reduce_to(const double* partial, int nb, double* out, int slot, hipStream_t st) {
@@ -2204,8 +2237,7 @@ int dxrl_pg_optimizer_step(int32_t device, const float* params, const float* gra
     AdamPackArgs a{params, grads, m1, m2, params_out, m1_out, m2_out, n, (float)lr, (float)beta1, (float)beta2,
                    (float)eps, (float)(1.0 - pow(beta1, (double)step)), (float)(1.0 - pow(beta2, (double)step)),
                    (float)max_norm, partial, kNb, gnorm2, static_cast<bf16*>(packed)};
-    const int64_t items = n > kW2 ? n : kW2;  // Adam elements / pack work items (kW2 >= every pack range)
-    hipLaunchKernelGGL(k_adam_pack, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_adam_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
     return launch_check("k_adam_pack");
 }
 

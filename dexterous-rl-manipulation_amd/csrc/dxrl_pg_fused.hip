@@ -77,6 +77,7 @@ struct FusedArgs {
     int64_t rows;
     const bf16* X;  // [rows][64], column 45 = 1
     const bf16 *W1, *W2, *W3, *W2T, *W3T;  // fragment-ordered streams (dxrl_pg.h kFr*)
+    const bf16* W3rm;  // the head's row-major bf16 copy [kOut][kHx] (16-row critic head)
     const float* b2;  // bias of hidden unit n: b2[n * kHx]
     const float* b3;  // bias of head row o:   b3[o * kHx]
     const float* logstd;
@@ -344,6 +345,12 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #ifndef DXRL_DH2_IN_DH1
 #define DXRL_DH2_IN_DH1 1
 #endif
+// The critic's value head on 16x16x32 tiles run by all eight waves (16 samples each, only head row
+// 0 nonzero) instead of 32x32x16 tiles on four waves (32 samples each, 31 dead head rows, four
+// waves idle): critic train 384 -> 375 us, critic values 215 -> 209 us (kernel-level A/B)
+#ifndef DXRL_CRITIC_HEAD16
+#define DXRL_CRITIC_HEAD16 1
+#endif
 #ifndef DXRL_HEAD_PF
 #define DXRL_HEAD_PF 1
 #endif
@@ -364,6 +371,8 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     using L = TileLds<kTR>;
     constexpr int kOffX = L::kOffX, kOffH1 = L::kOffH1, kOffH2 = L::kOffH2, kOffD = L::kOffD;
     constexpr int kHW = kTR / 32;  // waves running the heads (one 32-sample tile each)
+    // critic, 8 waves x 128 samples: every wave runs a 16-sample value head (DXRL_CRITIC_HEAD16)
+    constexpr bool kCH16 = DXRL_CRITIC_HEAD16 && kNet == 1 && kFW == 8 && kTR == 128;
     constexpr int kMT = kTR / 32;  // 32-sample MFMA tiles of a tile
     constexpr int kFThreads = 64 * kFW;
     constexpr int kNT = kH / 32 / kFW;  // 32-wide feature tiles per wave
@@ -500,6 +509,13 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
 #pragma unroll
             for (int q = 0; q < 16; ++q)
                 bk[q] = tanh_bias(((gf32*)b2)[(int64_t)(32 * bft + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
+            if constexpr (kCH16) {
+                if (kTrain) {
+                    const int64_t m16 = m0 + 16 * wave + (lane & 15);
+                    hv = p.ret[m16 < p.rows ? m16 : p.rows - 1];
+                }
+                return;
+            }
             if (!kTrain || __builtin_amdgcn_readfirstlane(wave) >= kHW) return;
             const int64_t mc = valid ? m : p.rows - 1;  // clamped: unconditional loads, no branch
             hv = (actor ? p.logp_old : p.ret)[mc];
@@ -544,7 +560,18 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         bf16x8 w3p[kW3P];
         float b3p[8];
         const gbf16x8* w3row = (const gbf16x8*)W3 + lane;  // fragment stream, feature tile 0
-        if (!kTrain || kHeadPf) {
+        // 16-row critic head: the 8 A fragments (head row lane & 15 -- only row 0, the value row,
+        // is loaded -- over k 32 ks + 8 (lane >> 4) ..) and the value bias, on every wave
+        bf16x8 w3h[kCH16 ? 8 : 1];
+        float b3h = 0.0f;
+        if constexpr (kCH16) {
+            const bf16* W3rm = opaque(p.W3rm);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                w3h[k] = (lane & 15) == 0 ? *(const gbf16x8*)(W3rm + 32 * k + 8 * (lane >> 4)) : zero8();
+            b3h = ((gf32*)b3)[0];
+        }
+        if (!kCH16 && (!kTrain || kHeadPf)) {
             if (wave < kHW) {
 #pragma unroll
                 for (int k = 0; k < kW3P; ++k) w3p[k] = w3row[64 * k];
@@ -561,11 +588,35 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // ---- head: wave w < kHW owns samples 32w .. 32w + 31 (lane: sample r, head rows of half h)
         // H1 tile -> HBM (B operand of the dW2 GEMM) by the waves that have no head tile; their
         // stores then retire while the head runs instead of holding the head's load waits
-        if constexpr (kTrain && kFW > kHW) {
+        if constexpr (kTrain && kFW > kHW && !kCH16) {
             if (wave >= kHW && p.h1_out)
                 copy_tile_out_n<64 * (kFW - kHW), kTR>(H1, p.h1_out, kHx, m0, p.rows, tid - 64 * kHW, diag);
         }
-        if (wave < kHW) {
+        if constexpr (kCH16) {
+            // wave w: samples 16 w .. 16 w + 15; V of sample 16 w + l in lane l < 16 (row 0, reg 0)
+            const int s16 = 16 * wave + (lane & 15);
+            const bf16* hb = H2 + s16 * kHp + 8 * (lane >> 4);
+            f32x4 a16 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a16 = mfma16(w3h[k], *reinterpret_cast<const bf16x8*>(hb + 32 * k), a16);
+            const int64_t m16 = m0 + s16;
+            const bool v16 = m16 < p.rows && lane < 16;
+            const float v = a16[0] + b3h;
+            float d0 = 0.0f;
+            if (!kTrain) {
+                if (v16) p.v_out[m16] = v;
+            } else if (v16) {
+                const float e = v - hv;  // hv: the return
+                d0 = from_bf16(to_bf16(p.vf2 * e * p.sc));
+                db3[0] += d0;
+                lsum[1] += e * e;
+            }
+            if (kTrain) {  // dout row of sample s16: d0 in column 0, zeros in 1..31 (lane >> 4: 8 columns)
+                bf16x8 dv = zero8();
+                if (lane < 16) dv[0] = to_bf16(d0);
+                *reinterpret_cast<bf16x8*>(D + s16 * kDp + 8 * (lane >> 4)) = dv;
+            }
+        } else if (wave < kHW) {
             f32x16 acc;
             zero_acc(acc);
             if constexpr (!kTrain) {
@@ -702,7 +753,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             STAMP(7);
             continue;
         }
-        if constexpr (kFW == kHW) {
+        if constexpr (kFW == kHW || kCH16) {
             if (p.h1_out) copy_tile_out_n<kFThreads, kTR>(H1, p.h1_out, kHx, m0, p.rows, tid, diag);
         }
         WPre<1> pw3t;  // dH2's one W3T fragment, ahead of the barrier
@@ -837,6 +888,30 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             }
     }
     if (tid < kH) part[kPartB2 + tid] = db2;
+    if constexpr (kCH16) {
+        // value-head bias gradient and value loss: lanes 0..15 of every wave, summed in
+        // (wave, lane) order
+        float* red = reinterpret_cast<float*>(lds);
+        double* lred = reinterpret_cast<double*>(lds + kOffH1);
+        red[tid] = db3[0];
+        lred[tid] = (double)lsum[1];
+        __syncthreads();
+        if (tid < 32) {
+            float sb = 0.0f;
+            if (tid == 0)
+                for (int w = 0; w < kFW; ++w)
+                    for (int rr = 0; rr < 16; ++rr) sb += red[64 * w + rr];
+            part[kPartW3 + tid * kHx + kH] = sb;  // bias column of head row tid (rows > 0: zero)
+            if (tid < 16) part[kPartLs + tid] = 0.0f;
+        } else if (tid == 33) {
+            double s = 0.0;
+            for (int w = 0; w < kFW; ++w)
+                for (int rr = 0; rr < 16; ++rr) s += lred[64 * w + rr];
+            p.loss[(int64_t)blockIdx.x * 4 + 1] = s;
+            for (int r = blockIdx.x + gridDim.x; r < p.loss_rows; r += gridDim.x) p.loss[(int64_t)r * 4 + 1] = 0.0;
+        }
+        return;
+    }
     float* red = reinterpret_cast<float*>(lds);              // [head lanes][16]
     double* lred = reinterpret_cast<double*>(lds + kOffH1);  // [head lanes][4]
     if (wave < kHW) {
@@ -1010,6 +1085,7 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     f.W3 = fr + kFrOffW3;
     f.W2T = fr + kFrOffW2T;
     f.W3T = fr + kFrOffW3T;
+    f.W3rm = w + (c ? kBfW3c : kBfW3a);
     f.b2 = a->params + o2 + kH;
     f.b3 = a->params + o3 + kH;
     f.logstd = a->params + kOffLogStd;

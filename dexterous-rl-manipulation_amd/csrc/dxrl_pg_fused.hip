@@ -351,6 +351,12 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #ifndef DXRL_CRITIC_HEAD16
 #define DXRL_CRITIC_HEAD16 1
 #endif
+// The actor's head on 16x16x32 tiles run by all eight waves (16 samples each, head rows 0..15; a
+// sample's 16 log-density terms gathered by shuffles and summed in action order as before):
+// actor train 427.6 -> 423.3 us (kernel-level A/B), 249 -> 231 VGPRs
+#ifndef DXRL_ACTOR_HEAD16
+#define DXRL_ACTOR_HEAD16 1
+#endif
 #ifndef DXRL_HEAD_PF
 #define DXRL_HEAD_PF 1
 #endif
@@ -373,6 +379,8 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     constexpr int kHW = kTR / 32;  // waves running the heads (one 32-sample tile each)
     // critic, 8 waves x 128 samples: every wave runs a 16-sample value head (DXRL_CRITIC_HEAD16)
     constexpr bool kCH16 = DXRL_CRITIC_HEAD16 && kNet == 1 && kFW == 8 && kTR == 128;
+    constexpr bool kAH16 = DXRL_ACTOR_HEAD16 && kNet == 0 && kTrain && kFW == 8 && kTR == 128;
+    constexpr bool kH16 = kCH16 || kAH16;
     constexpr int kMT = kTR / 32;  // 32-sample MFMA tiles of a tile
     constexpr int kFThreads = 64 * kFW;
     constexpr int kNT = kH / 32 / kFW;  // 32-wide feature tiles per wave
@@ -516,6 +524,13 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 }
                 return;
             }
+            if constexpr (kAH16) {  // sample 16 w + (lane & 15), actions 4 (lane >> 4) .. + 3
+                const int64_t m16 = m0 + 16 * wave + (lane & 15), mc = m16 < p.rows ? m16 : p.rows - 1;
+                hv = p.logp_old[mc];
+                a0 = *reinterpret_cast<const float4*>(p.act + mc * kActPad + 4 * (lane >> 4));
+                adv = p.adv[mc];
+                return;
+            }
             if (!kTrain || __builtin_amdgcn_readfirstlane(wave) >= kHW) return;
             const int64_t mc = valid ? m : p.rows - 1;  // clamped: unconditional loads, no branch
             hv = (actor ? p.logp_old : p.ret)[mc];
@@ -562,8 +577,13 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         const gbf16x8* w3row = (const gbf16x8*)W3 + lane;  // fragment stream, feature tile 0
         // 16-row critic head: the 8 A fragments (head row lane & 15 -- only row 0, the value row,
         // is loaded -- over k 32 ks + 8 (lane >> 4) ..) and the value bias, on every wave
-        bf16x8 w3h[kCH16 ? 8 : 1];
+        bf16x8 w3h[kH16 ? 8 : 1];
         float b3h = 0.0f;
+        if constexpr (kAH16) {  // head rows lane & 15 (0..14 the means, 15 zero)
+            const bf16* W3rm = opaque(p.W3rm) + (lane & 15) * kHx + 8 * (lane >> 4);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w3h[k] = *(const gbf16x8*)(W3rm + 32 * k);
+        }
         if constexpr (kCH16) {
             const bf16* W3rm = opaque(p.W3rm);
 #pragma unroll
@@ -571,7 +591,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 w3h[k] = (lane & 15) == 0 ? *(const gbf16x8*)(W3rm + 32 * k + 8 * (lane >> 4)) : zero8();
             b3h = ((gf32*)b3)[0];
         }
-        if (!kCH16 && (!kTrain || kHeadPf)) {
+        if (!kH16 && (!kTrain || kHeadPf)) {
             if (wave < kHW) {
 #pragma unroll
                 for (int k = 0; k < kW3P; ++k) w3p[k] = w3row[64 * k];
@@ -588,7 +608,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // ---- head: wave w < kHW owns samples 32w .. 32w + 31 (lane: sample r, head rows of half h)
         // H1 tile -> HBM (B operand of the dW2 GEMM) by the waves that have no head tile; their
         // stores then retire while the head runs instead of holding the head's load waits
-        if constexpr (kTrain && kFW > kHW && !kCH16) {
+        if constexpr (kTrain && kFW > kHW && !kH16) {
             if (wave >= kHW && p.h1_out)
                 copy_tile_out_n<64 * (kFW - kHW), kTR>(H1, p.h1_out, kHx, m0, p.rows, tid - 64 * kHW, diag);
         }
@@ -616,6 +636,70 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 if (lane < 16) dv[0] = to_bf16(d0);
                 *reinterpret_cast<bf16x8*>(D + s16 * kDp + 8 * (lane >> 4)) = dv;
             }
+        } else if constexpr (kAH16) {
+            // wave w: samples 16 w .. + 15; lane l holds head rows o = 4 (l >> 4) + i of sample l & 15
+            const int s16 = 16 * wave + (lane & 15), g4 = lane >> 4;
+            const bf16* hb = H2 + s16 * kHp + 8 * g4;
+            f32x4 a16 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a16 = mfma16(w3h[k], *reinterpret_cast<const bf16x8*>(hb + 32 * k), a16);
+            const int64_t m16 = m0 + s16;
+            const bool v16 = m16 < p.rows;
+            float mu[4], a[4], lsv[4], iv2[4], t[4], d[4];
+            a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int o = 4 * g4 + i;
+                lsv[i] = o < kAct ? ((gf32*)logstd)[o] : 0.0f;
+                iv2[i] = __expf(-2.0f * lsv[i]);
+                mu[i] = a16[i] + ((gf32*)b3)[(int64_t)o * kHx];
+                const float z = (a[i] - mu[i]) * __expf(-lsv[i]);
+                t[i] = o < kAct ? -0.5f * z * z - lsv[i] - 0.5f * kLog2PiF : 0.0f;
+                d[i] = 0.0f;
+            }
+            // log pi(a|s): the sample's 15 terms gathered from its four lanes, summed in action order
+            float tt[16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) tt[4 * g + i] = __shfl(t[i], (lane & 15) + 16 * g);
+            float lp = 0.0f;
+#pragma unroll
+            for (int o = 0; o < kAct; ++o) lp += tt[o];
+            const float lo = hv;
+            const float ratio = __expf(lp - lo);
+            const float A = (float)(((double)adv - adv_mean) * adv_inv);
+            const float s1 = ratio * A;
+            const float rc = fminf(fmaxf(ratio, 1.0f - p.clip_eps), 1.0f + p.clip_eps);
+            const float s2 = rc * A;
+            float g = 0.0f;
+            if (s1 <= s2 || ratio == rc) g = -A * ratio;  // d(-min(s1, s2)) / d logp
+            g *= p.sc;
+            if (v16) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int o = 4 * g4 + i;
+                    if (o < kAct) {
+                        const float dd = a[i] - mu[i];
+                        d[i] = from_bf16(to_bf16(g * dd * iv2[i]));  // dlogp/dmu = (a - mu) / sigma^2
+                        dls[i] += g * (dd * dd * iv2[i] - 1.0f);       // dlogp/dlogstd
+                        db3[i] += d[i];
+                    }
+                }
+                if (g4 == 0) {
+                    lsum[0] += -fminf(s1, s2);
+                    lsum[2] += fabsf(ratio - 1.0f) > p.clip_eps ? 1.0f : 0.0f;
+                    lsum[3] += lo - lp;
+                }
+            }
+            bf16x4 dv, zv;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                dv[i] = to_bf16(d[i]);
+                zv[i] = (bf16)0.0f;
+            }
+            *reinterpret_cast<bf16x4*>(D + s16 * kDp + 4 * g4) = dv;        // head rows 4 g4 .. + 3
+            *reinterpret_cast<bf16x4*>(D + s16 * kDp + 16 + 4 * g4) = zv;   // rows 16 .. 31: zero
         } else if (wave < kHW) {
             f32x16 acc;
             zero_acc(acc);
@@ -753,7 +837,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             STAMP(7);
             continue;
         }
-        if constexpr (kFW == kHW || kCH16) {
+        if constexpr (kFW == kHW || kH16) {
             if (p.h1_out) copy_tile_out_n<kFThreads, kTR>(H1, p.h1_out, kHx, m0, p.rows, tid, diag);
         }
         WPre<1> pw3t;  // dH2's one W3T fragment, ahead of the barrier
@@ -909,6 +993,43 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 for (int rr = 0; rr < 16; ++rr) s += lred[64 * w + rr];
             p.loss[(int64_t)blockIdx.x * 4 + 1] = s;
             for (int r = blockIdx.x + gridDim.x; r < p.loss_rows; r += gridDim.x) p.loss[(int64_t)r * 4 + 1] = 0.0;
+        }
+        return;
+    }
+    if constexpr (kAH16) {
+        // head rows o = 4 g + i of lanes 16 g .. 16 g + 15 of every wave, summed in (wave, lane)
+        // order; the loss terms over every lane in thread order
+        float* red = reinterpret_cast<float*>(lds);              // [512][8]: dls[0..3], db3[0..3]
+        double* lred = reinterpret_cast<double*>(lds + kOffH1);  // [512][4]
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            red[tid * 8 + i] = dls[i];
+            red[tid * 8 + 4 + i] = db3[i];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lred[tid * 4 + k] = (double)lsum[k];
+        __syncthreads();
+        if (tid < 32) {
+            const int o = tid, g = (o >> 2) & 3, i = o & 3;
+            float sl = 0.0f, sb = 0.0f;
+            if (o < 16) {
+                for (int w = 0; w < kFW; ++w)
+                    for (int rr = 0; rr < 16; ++rr) {
+                        const int t = 64 * w + 16 * g + rr;
+                        sl += red[t * 8 + i];
+                        sb += red[t * 8 + 4 + i];
+                    }
+            }
+            part[kPartW3 + o * kHx + kH] = sb;  // bias column of the head
+            if (o < 16) part[kPartLs + o] = sl;
+        } else if (tid < 36) {
+            const int k = tid - 32;
+            if (k != 1) {
+                double s = 0.0;
+                for (int t = 0; t < kFThreads; ++t) s += lred[t * 4 + k];
+                p.loss[(int64_t)blockIdx.x * 4 + k] = s;
+                for (int r = blockIdx.x + gridDim.x; r < p.loss_rows; r += gridDim.x) p.loss[(int64_t)r * 4 + k] = 0.0;
+            }
         }
         return;
     }

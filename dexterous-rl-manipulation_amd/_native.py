@@ -141,6 +141,8 @@ _SIGS = {
     "dxrl_env_reset": (C.c_int, [_P, _P, _P, _P, _P]),
     "dxrl_env_step": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "dxrl_env_observe": (C.c_int, [_P, _P, _P]),
+    "dxrl_reward_compute": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, _P, _P,
+                                      _P, _P, _P]),
     "dxrl_env_set_max_episode_steps": (C.c_int, [_P, C.c_int32]),
     "dxrl_learner_layout_for": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(LearnerLayout)]),
     "dxrl_learner_init": (C.c_int, [C.c_int32, C.c_int32, _P, _P]),
@@ -156,6 +158,7 @@ _SIGS = {
     "dxrl_pg_pack_weights": (C.c_int, [_I32, _P, _P, _P]),
     "dxrl_pg_rollout": (C.c_int, [_P, _P, _P, C.POINTER(PgRolloutArgs), _P]),
     "dxrl_pg_gae": (C.c_int, [_I32, _P, _P, _P, _I64, _I64, _F64, _F64, _P, _P, _P, _P, _P]),
+    "dxrl_pg_gae_partial_doubles": (C.c_int, [_I64, _I64, C.POINTER(_I64)]),
     "dxrl_pg_adv_finalize": (C.c_int, [_I32, _I32, _P, _I64, _P, _P, _P]),
     "dxrl_pg_adv_combine": (C.c_int, [_I32, _P, _I32, _P, _P]),
     "dxrl_pg_heads": (C.c_int, [_I32, C.POINTER(PgHeadsArgs), _P]),
@@ -210,6 +213,13 @@ def check(rc: int, what: str = ""):
 
 def call(name: str, *args):
     check(getattr(lib(), name)(*args), name)
+
+
+def gae_partial_doubles(num_envs: int, horizon: int) -> int:
+    """f64 elements of dxrl_pg_gae's `partial` scratch (include/dxrl.h)."""
+    out = C.c_int64()
+    call("dxrl_pg_gae_partial_doubles", num_envs, horizon, C.byref(out))
+    return out.value
 
 
 def ptr(t) -> int | None:

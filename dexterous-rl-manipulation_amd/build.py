@@ -50,13 +50,43 @@ def asan_runtime() -> str:
     return hits[-1] if hits else ""
 
 
+def _jobs() -> int:
+    try:
+        return max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 1), 16))
+    except ValueError:
+        return 1
+
+
 def build_native(force: bool = False, verbose: bool = False, asan: bool = False) -> str:
+    """One object per translation unit (compiled in parallel, each rebuilt only when it or a
+    header changed), then one link.  Every TU carries its own gfx950 code object (no -fgpu-rdc),
+    as the single-command build did."""
+    from concurrent.futures import ThreadPoolExecutor
     out = ASAN_OUT if asan else OUT
     if not force and os.path.exists(out) and all(os.path.getmtime(f) <= os.path.getmtime(out) for f in _inputs()):
         return out
-    cmd = [HIPCC, *FLAGS, *(ASAN_FLAGS if asan else []), "-o", out + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
+    objdir = os.path.join(PKG_DIR, "_obj_asan" if asan else "_obj")
+    os.makedirs(objdir, exist_ok=True)
+    extra = ASAN_FLAGS if asan else []
+    hdr_t = max(os.path.getmtime(f) for f in _inputs() if not f.endswith(".hip"))
+    compile_flags = [f for f in FLAGS if f != "-shared"]
+
+    def obj(src):
+        o = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        s = os.path.join(CSRC, src)
+        if force or not os.path.exists(o) or os.path.getmtime(o) < max(hdr_t, os.path.getmtime(s)):
+            cmd = [HIPCC, *compile_flags, *extra, "-c", "-o", o + ".tmp", s]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True, cwd=CSRC)
+            os.replace(o + ".tmp", o)
+        return o
+
+    with ThreadPoolExecutor(_jobs()) as ex:
+        objs = list(ex.map(obj, SOURCES))
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *extra, "-o", out + ".tmp", *objs]
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(out + ".tmp", out)
     return out

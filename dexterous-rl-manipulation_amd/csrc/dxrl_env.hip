@@ -186,6 +186,65 @@ __global__ void k_observe(EnvSoA s, float* __restrict__ obs) {
     write_obs(e, obs + i * kObs);
 }
 
+// RewardShaping.compute / SparseReward.compute on caller-given inputs (RS:50-99, RS:205-242), one
+// thread per item.  The dense terms come from dense_reward() -- the function every step kernel
+// fuses -- fed with the min fingertip distance of the GIVEN finger_tips (RS:111-113,
+// np.linalg.norm axis=1 = sqrt((dx^2 + dy^2) + dz^2) in f64) and the contact mask contacts > 0.5
+// (RS:130).  Stability (RS:166-187) is restated on the f32 contact values themselves
+// (np.abs(c - prev) summed in order, / len, 1 - x, clip), which for the env's 0 / 1 contacts is
+// dense_reward's bitmask form bit for bit and also covers fractional contacts; prev / has_prev
+// are the plugin's prev_contacts state, updated in place.
+__global__ void k_reward_compute(int64_t count, bool dense, Weights w, const float* __restrict__ jp,
+                                 const double* __restrict__ tips, const double* __restrict__ op,
+                                 const float* __restrict__ contacts, float* __restrict__ prev,
+                                 uint8_t* __restrict__ has_prev, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    float c[kF];
+    uint32_t mask = 0;
+#pragma unroll
+    for (int f = 0; f < kF; ++f) {
+        c[f] = contacts[i * kF + f];
+        mask |= (c[f] > 0.5f ? 1u : 0u) << f;
+    }
+    double* o = out + i * 5;
+    if (!dense) {  // RS:228-242
+        o[0] = __popc(mask) >= 3 ? 1.0 : -0.01;
+        o[1] = o[2] = o[3] = o[4] = 0.0;
+        return;
+    }
+    double dmin = 0.0;
+#pragma unroll
+    for (int f = 0; f < kF; ++f) {
+        const double* t = tips + (i * kF + f) * 3;
+        const double dx = t[0] - op[i * 3 + 0], dy = t[1] - op[i * 3 + 1], dz = t[2] - op[i * 3 + 2];
+        const double d = sqrt((dx * dx + dy * dy) + dz * dz);
+        dmin = (f == 0 || d < dmin) ? d : dmin;  // np.min
+    }
+    Env e{};
+#pragma unroll
+    for (int k = 0; k < kD; ++k) e.jp[k] = jp[i * kD + k];
+    e.flags = 0;  // stability is taken from the float restatement below
+    double comp[4];
+    (void)dense_reward(e, mask, dmin, w, comp);
+    float st = 0.0f;
+    if (has_prev[i]) {
+        float ch = 0.0f;
+#pragma unroll
+        for (int f = 0; f < kF; ++f) ch = ch + fabsf(c[f] - prev[i * kF + f]);
+        st = clipf(1.0f - ch / (float)kF, 0.0f, 1.0f);
+    }
+#pragma unroll
+    for (int f = 0; f < kF; ++f) prev[i * kF + f] = c[f];
+    has_prev[i] = 1;
+    comp[3] = (double)st;
+    o[0] = ((w.w_dist * comp[0] + w.w_con * comp[1]) + w.w_clo * comp[2]) + w.w_st * comp[3];  // RS:86-91
+    o[1] = comp[0];
+    o[2] = comp[1];
+    o[3] = comp[2];
+    o[4] = comp[3];
+}
+
 static int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
 int layout_for(const dxrl_env_config* cfg, dxrl_env_layout* L) {
@@ -382,6 +441,31 @@ int dxrl_env_set_max_episode_steps(dxrl_env* env, int32_t max_episode_steps) {
     DXRL_REQUIRE(env, "null env");
     env->cfg.max_episode_steps = max_episode_steps;
     return DXRL_OK;
+}
+
+int dxrl_reward_compute(int32_t device, int32_t reward_type, const double* weights, int64_t count,
+                        int32_t num_fingers, int32_t joints_per_finger, const float* joint_positions,
+                        const double* finger_tips, const double* object_position, const float* contacts,
+                        float* prev_contacts, uint8_t* has_prev, double* out, void* stream) {
+    DXRL_REQUIRE(reward_type == DXRL_REWARD_DENSE || reward_type == DXRL_REWARD_SPARSE,
+                 "reward_type must be DXRL_REWARD_DENSE or DXRL_REWARD_SPARSE");
+    if (num_fingers != kF || joints_per_finger != kJ) {
+        set_error("this build compiles num_fingers=%d, joints_per_finger=%d (got %d, %d)", kF, kJ, num_fingers,
+                  joints_per_finger);
+        return DXRL_E_UNSUPPORTED;
+    }
+    DXRL_REQUIRE(count >= 0, "count must be >= 0");
+    DXRL_REQUIRE(contacts && out, "null contacts/out");
+    const bool dense = reward_type == DXRL_REWARD_DENSE;
+    DXRL_REQUIRE(!dense || (weights && joint_positions && finger_tips && object_position && prev_contacts && has_prev),
+                 "the dense reward needs weights, joint_positions, finger_tips, object_position and the prev state");
+    if (count == 0) return DXRL_OK;
+    const Weights w = dense ? Weights{weights[0], weights[1], weights[2], weights[3]} : Weights{0.0, 0.0, 0.0, 0.0};
+    DeviceGuard g(device);
+    hipLaunchKernelGGL(k_reward_compute, dim3((unsigned)((count + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       as_stream(stream), count, dense, w, joint_positions, finger_tips, object_position, contacts,
+                       prev_contacts, has_prev, out);
+    return launch_check("k_reward_compute");
 }
 
 int dxrl_env_observe(dxrl_env* env, float* obs, void* stream) {

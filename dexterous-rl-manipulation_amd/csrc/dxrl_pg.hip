@@ -2152,10 +2152,19 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
     return DXRL_OK;
 }
 
+int dxrl_pg_gae_partial_doubles(int64_t num_envs, int64_t horizon, int64_t* doubles) {
+    DXRL_REQUIRE(doubles && num_envs >= 1 && horizon >= 1, "bad argument");
+    // one Moments triple per workgroup; k_gae_lds (16 envs per workgroup) launches the most
+    static_assert(kGlEnvs <= kGaeThreads, "k_gae_lds must be the kernel with the most workgroups");
+    *doubles = 3 * ((num_envs + kGlEnvs - 1) / kGlEnvs);
+    return DXRL_OK;
+}
+
 int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const float* values, int64_t num_envs,
                 int64_t horizon, double gamma, double lam, float* adv, float* ret, double* partial, double* stats,
                 void* stream) {
     DXRL_REQUIRE(rew && done && values && adv && ret && partial && stats, "null argument");
+    DXRL_REQUIRE(num_envs >= 1 && horizon >= 1, "num_envs and horizon must be >= 1");
     DeviceGuard g(device);
     hipStream_t st = as_stream(stream);
     static const bool seq = [] {  // A/B: k_gae, the chunked-load scan (DXRL_GAE_SEQ=1)

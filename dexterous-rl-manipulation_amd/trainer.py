@@ -193,7 +193,8 @@ class PGTrainer:
         self.adv, self.ret = z(M), z(M)
         self.stats = torch.zeros(8, dtype=torch.float64, device=d)
         self.moments_all = torch.zeros(self.world, 3, dtype=torch.float64, device=d)  # ranks' stats[5..7]
-        nb = max(1024, (M + 255) // 256, 3 * ((n + 31) // 32))  # GAE: one (n, mean, M2) per 32-env block
+        # shared f64 scratch: the optimiser's 512 grad-norm partials and dxrl_pg_gae's moment triples
+        nb = max(512, N.gae_partial_doubles(n, T))
         self.partial = torch.zeros(nb, dtype=torch.float64, device=d)
         self.dH2 = z(M, H, dt=bf)
         self.splits = max(1, min(cfg.splitk_target_blocks // 3, M // 1024))  # dW2: one workgroup per CU

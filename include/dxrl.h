@@ -127,6 +127,27 @@ int dxrl_env_reset(dxrl_env* env, const uint8_t* mask, const double* draws, floa
 int dxrl_env_step(dxrl_env* env, const float* actions, float* obs, double* reward,
                   uint8_t* terminated, uint8_t* truncated, double* components, void* stream);
 
+/* The reward plugins' own entry point, for callers outside env.step():
+ *   rewards/reward_shaping.py:50-99   RewardShaping.compute(joint_positions, finger_tips,
+ *                                     object_position, contacts, num_fingers, joints_per_finger)
+ *   rewards/reward_shaping.py:205-242 SparseReward.compute(...)
+ * as called at envs/manipulation_env.py:318-325, for `count` independent items.  The dense
+ * terms are the step kernels' own dense_reward (csrc/dxrl_device.h) on the given inputs.
+ *   weights          HOST f64 [4] distance, contact, closure, stability (dense only);
+ *                    every other array is device memory
+ *   joint_positions  f32 [count][15]      (the env's f32 joint array, ME:143-145)
+ *   finger_tips      f64 [count][5][3]    (ME:296-303)
+ *   object_position  f64 [count][3]
+ *   contacts         f32 [count][5]       (ME:310; > 0.5 counts as a contact)
+ *   prev_contacts    f32 [count][5], has_prev u8 [count]: RewardShaping.prev_contacts (None ==
+ *                    has_prev 0), read and updated in place as RS:172-185 does (dense only)
+ *   out              f64 [count][5]: total, distance, contact, closure, stability
+ * num_fingers / joints_per_finger must be this build's 5 / 3 (DXRL_E_UNSUPPORTED otherwise). */
+int dxrl_reward_compute(int32_t device, int32_t reward_type, const double* weights, int64_t count,
+                        int32_t num_fingers, int32_t joints_per_finger, const float* joint_positions,
+                        const double* finger_tips, const double* object_position, const float* contacts,
+                        float* prev_contacts, uint8_t* has_prev, double* out, void* stream);
+
 /* Recompute the observation of the current state (envs/manipulation_env.py:254-264). */
 int dxrl_env_observe(dxrl_env* env, float* obs, void* stream);
 
@@ -285,14 +306,21 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
  * moments stats[5] = T N, stats[6] = mean(adv), stats[7] = sum of squared deviations, and
  * stats[0..4] as dxrl_pg_adv_combine(stats + 5, world = 1) would (single rank: no second call)
  * (per-env sums about the env's own first value, merged with Chan et al.'s pairwise update
- * in a fixed order: no sum(a^2) - mean sum(a) cancellation).  horizon <= 256: a segmented scan
- * over time (8 segments per env, boundary values from the composed segment maps: adv within a
- * few f32 ulps of the sequential scan); longer horizons: one sequential scan per env.
- * partial: f64 [3 ceil(N / 32)];
+ * in a fixed order: no sum(a^2) - mean sum(a) cancellation).
+ * The scan is the SEQUENTIAL recurrence A_t = delta_t + (gamma lambda)(1 - d_t) A_{t+1} per env,
+ * bit-exact against a one-env-at-a-time reverse loop in that operation order:
+ *   horizon * 208 B <= 152 KiB (T <= 748): k_gae_lds -- a 256-thread workgroup per 16 envs
+ *     stages the horizon in LDS with all its threads (delta_t computed in parallel), one lane per
+ *     env runs the two-op chain, all threads store adv / ret;  ceil(N / 16) workgroups;
+ *   longer horizons: k_gae -- one thread per env, 64-env workgroups;  ceil(N / 64) workgroups.
+ * Each workgroup writes one (count, mean, M2) triple into `partial`.
+ * partial: f64 [dxrl_pg_gae_partial_doubles(N, T)] (= 3 ceil(N / 16), enough for either kernel);
  * stats: f64 [8]. */
 int dxrl_pg_gae(int32_t device, const float* rew, const uint8_t* done, const float* values, int64_t num_envs,
                 int64_t horizon, double gamma, double lam, float* adv, float* ret, double* partial, double* stats,
                 void* stream);
+/* f64 elements of dxrl_pg_gae's `partial` scratch for (num_envs, horizon) (host-only query). */
+int dxrl_pg_gae_partial_doubles(int64_t num_envs, int64_t horizon, int64_t* doubles);
 /* Global advantage statistics from every rank's (count, mean, M2) triple -- moments f64
  * [world][3] in rank order (all-gathered stats[5..7]) -- merged in rank order into
  * stats[0] count, [1] sum, [2] mean, [3] sum of squared deviations, [4] unbiased std (what the

@@ -289,6 +289,45 @@ def oracle_noisy_obs(obs, noise):
     return (obs + np.asarray(noise).astype(np.float32)).astype(np.float32)
 
 
+# ---------------------------------------------------------------- reward plugins on given inputs
+def oracle_reward_compute(joint_positions, finger_tips, object_position, contacts, prev_contacts, weights,
+                          dense: bool = True, num_fingers: int = F, joints_per_finger: int = J):
+    """RewardShaping.compute (rewards/reward_shaping.py:50-187) / SparseReward.compute (:205-242)
+    on caller-given arrays, with numpy's own functions in the reference's dtypes (f32 joints and
+    contacts, f64 tips and object position).  Returns ((total, distance, contact, closure,
+    stability), new prev_contacts); prev_contacts None = the first call after reset()."""
+    c = np.asarray(contacts, np.float32)
+    n_con = np.sum(c > 0.5)
+    if not dense:
+        return ((1.0 if n_con >= 3 else -0.01), 0.0, 0.0, 0.0, 0.0), prev_contacts
+    jp = np.asarray(joint_positions, np.float32)
+    d = np.linalg.norm(np.asarray(finger_tips, np.float64) - np.asarray(object_position, np.float64), axis=1)
+    dist = float(np.exp(-5.0 * np.min(d)))                        # :111-118
+    con = float(n_con / num_fingers)                               # :130-136
+    scores = []
+    for f in range(num_fingers):                                   # :149-164
+        fj = jp[f * joints_per_finger:(f + 1) * joints_per_finger]
+        scores.append(-np.sum(fj[fj < 0]))
+    clo = float(np.clip(np.mean(scores) / num_fingers, 0.0, 1.0))
+    if prev_contacts is None:                                      # :172-175
+        st = 0.0
+    else:                                                          # :178-187
+        ch = np.sum(np.abs(c - np.asarray(prev_contacts, np.float32)))
+        st = float(np.clip(1.0 - (ch / len(c)), 0.0, 1.0))
+    w = weights
+    total = w[0] * dist + w[1] * con + w[2] * clo + w[3] * st     # :86-91
+    return (total, dist, con, clo, st), c.copy()
+
+
+def oracle_finger_tips(jp):
+    """envs/manipulation_env.py:296-303: tip_f = zeros(3) + f32(sum(joints of f)) * 0.1 -> f64 [5][3]."""
+    jp = np.asarray(jp, np.float32)
+    out = np.empty((F, 3), np.float64)
+    for f in range(F):
+        out[f] = np.array([0.0, 0.0, 0.0]) + np.sum(jp[f * J:(f + 1) * J]) * 0.1
+    return out
+
+
 # ---------------------------------------------------------------- evaluation episode programs
 POLICY_SIMPLE, POLICY_HEURISTIC, POLICY_RANDOM = 0, 1, 2
 

@@ -211,7 +211,41 @@ def test_fused_noise_streams(run):
         assert (err <= sig32 * (1e-4 + 1e-4 * np.abs(z))).all(), (name, stream, err.max())
 
 
-def test_normalisation_large_mean(pkg):
+@pytest.mark.parametrize("name", CONFIGS)
+def test_benched_rollout_equals_parity_instantiation(pkg, name):
+    """The bench runs k_pg_rollout_ws<noise, kDiag=false>; the oracle tests above check
+    <noise, true> (selected by the parity tapes).  From one snapshot of the env state slab and
+    the open-episode returns, the rollout runs once with the tapes and once without: every
+    tape (obs / act / log pi / rew / done / episode codes), the per-env sums, the episode
+    records and the env state after the launch are bit-identical.  Second iteration: the
+    state going in has mid-episode envs and the Philox counters have moved."""
+    dev = torch.device("cuda", 0)
+    env, tr = pkg.workloads.build_pg_workload(name, dev, record_cap=8)
+    tr.rollout()  # advance into mid-episode state
+    tr.iteration_index += 1
+    if tr.ep_code is None:
+        tr.ep_code = torch.zeros(tr.M, dtype=torch.int16, device=dev)
+    torch.cuda.synchronize()
+    snap, ret0 = env.state.clone(), tr.ep_ret.clone()
+    outs = []
+    for tapes in (True, False):
+        env.state.copy_(snap)
+        tr.ep_ret.copy_(ret0)
+        for t in (tr.obs_rm, tr.act, tr.logp, tr.rew, tr.done, tr.ep_count, tr.ep_sum_ret, tr.ep_sum_len, tr.ep_succ,
+                  tr.rec_return, tr.rec_length, tr.rec_success, tr.rec_end, tr.ep_code):
+            t.fill_(0x5A if t.dtype in (torch.uint8,) else 7)
+        tr.applied_act = torch.zeros(tr.M, 16, device=dev) if tapes else None
+        tr.dyn_noise_tape = torch.zeros(tr.M, 16, device=dev) if tapes else None
+        tr.obs_noise_tape = torch.zeros(tr.M + tr.n, 48, device=dev) if tapes else None
+        tr.rollout()
+        torch.cuda.synchronize()
+        outs.append({k: getattr(tr, k).clone() for k in (
+            "obs_rm", "act", "logp", "rew", "done", "ep_count", "ep_sum_ret", "ep_sum_len", "ep_succ", "rec_return",
+            "rec_length", "rec_success", "rec_end", "ep_code", "ep_ret")} | {"state": env.state.clone()})
+    a, b = outs
+    for k in a:
+        assert a[k].view(torch.uint8).equal(b[k].view(torch.uint8)), (name, k)
+    assert int(a["ep_count"].sum()) > 0
     """The normalisation moments with |mean| / std > 1e3 (every step its own episode,
     A = r - V, rewards shifted by 1e4): a one-pass sum(a^2) - mean sum(a) lost 2.8e-6 of
     the std here; the merged (count, mean, M2) moments (k_gae / k_gae_sums /

@@ -424,12 +424,18 @@ def test_optimizer_step_matches_torch_clip_and_adam(pkg):
 
 
 @pytest.mark.parametrize("n,T,p_done", [(100, 1, 0.1), (64, 7, 0.0), (4096, 25, 0.05), (96, 33, 0.3),
-                                        (4096, 200, 0.02), (130, 256, 0.0), (70, 300, 0.05)])
+                                        (4096, 200, 0.02), (130, 256, 0.0), (70, 300, 0.05),
+                                        # many envs, short horizons: the partial buffer's worst cases
+                                        (8192, 32, 0.05), (6000, 8, 0.1), (65536, 1, 0.2),
+                                        # past the LDS staging limit: the k_gae fallback
+                                        (200, 800, 0.01)])
 def test_gae_lds_scan_matches_sequential_reference(pkg, n, T, p_done):
     """dxrl_pg_gae (k_gae_lds: the horizon staged in LDS by the whole workgroup, one lane per env
-    running the recurrence) gives pg_reference.gae's adv / ret (the kernel's op order) bit for
-    bit, and the moments (count, mean, M2) a two-pass f64 reduction's to 1e-9.  Ragged env
-    counts, no dones and dense dones, horizons from 1 to 300."""
+    running the recurrence; k_gae past T = 748) gives pg_reference.gae's adv / ret (the kernel's
+    op order) bit for bit, and the moments (count, mean, M2) a two-pass f64 reduction's to 1e-9.
+    Ragged env counts, no dones and dense dones, horizons from 1 to 800.  `partial` is sized by
+    dxrl_pg_gae_partial_doubles exactly, with a NaN canary block behind it that must survive
+    (one Moments triple per workgroup; the header once documented half of that)."""
     from dexterous_rl_manipulation_amd import _native as N
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(n * 1000 + T)
@@ -437,11 +443,15 @@ def test_gae_lds_scan_matches_sequential_reference(pkg, n, T, p_done):
     V = torch.randn((T + 1) * n, generator=g, device=dev) * 3.0
     done = (torch.rand(T * n, generator=g, device=dev) < p_done).to(torch.uint8)
     adv, ret = torch.empty_like(rew), torch.empty_like(rew)
-    part = torch.zeros(max(1024, 3 * ((n + 31) // 32)), dtype=torch.float64, device=dev)
+    need = N.gae_partial_doubles(n, T)
+    assert need == 3 * ((n + 15) // 16)
+    canary = 4096
+    part = torch.full((need + canary,), float("nan"), dtype=torch.float64, device=dev)
     stats = torch.zeros(8, dtype=torch.float64, device=dev)
     N.call("dxrl_pg_gae", 0, N.ptr(rew), N.ptr(done), N.ptr(V), n, T, 0.99, 0.95, N.ptr(adv), N.ptr(ret),
            N.ptr(part), N.ptr(stats), N.stream_of(dev))
     torch.cuda.synchronize()
+    assert torch.isnan(part[need:]).all(), "dxrl_pg_gae wrote past dxrl_pg_gae_partial_doubles"
     a_ref, r_ref = R.gae(rew, done, V, n, T, 0.99, 0.95)
     assert torch.equal(adv, a_ref) and torch.equal(ret, r_ref)
     a = adv.double()

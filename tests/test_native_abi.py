@@ -62,6 +62,15 @@ def test_layout_is_aligned_and_sized(native):
     assert lay.jv - lay.jp >= 4 * 15 * 4099 and lay.total_bytes > lay.curricula
 
 
+def test_gae_partial_size_query(native):
+    """dxrl_pg_gae's moment scratch: one (count, mean, M2) f64 triple per 16-env workgroup of
+    k_gae_lds, the kernel with the most workgroups (include/dxrl.h)."""
+    for n, T in ((1, 1), (16, 200), (17, 200), (8192, 32), (6000, 8), (65536, 1), (200, 800)):
+        assert native.gae_partial_doubles(n, T) == 3 * ((n + 15) // 16)
+    with pytest.raises(ValueError):
+        native.gae_partial_doubles(0, 5)
+
+
 STRUCTS = ["dxrl_curriculum", "dxrl_env_config", "dxrl_env_layout", "dxrl_learner_layout", "dxrl_learner_config",
            "dxrl_rollout_io", "dxrl_pg_rollout_args", "dxrl_pg_heads_args",
            "dxrl_pg_fused_args", "dxrl_eval_segment", "dxrl_eval_args", "dxrl_sched_args"]

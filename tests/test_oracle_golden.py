@@ -161,3 +161,23 @@ def test_vectorised_philox_matches_scalar():
                 rad = math.sqrt(-2.0 * math.log(ua))
                 assert z[j, 4 * b + 2 * h] == rad * math.cos(2 * math.pi * ub)
                 assert z[j, 4 * b + 2 * h + 1] == rad * math.sin(2 * math.pi * ub)
+
+
+@pytest.mark.parametrize("case", ENV_CASES, ids=lambda c: f"c{c['index']}-{c['cfg']}-{c['reward']}")
+def test_reward_plugin_restatement_matches_golden(case):
+    """oracle_reward_compute (RewardShaping / SparseReward.compute on given arrays) reproduces
+    every recorded reward and component from the trace's own inputs (golden_io
+    .reward_plugin_inputs), the state carried across steps and cleared at each reset; and
+    oracle_finger_tips equals the fixture-derived tips."""
+    from oracle.dx_oracle import oracle_finger_tips, oracle_reward_compute
+    z = G.env_case(case["index"])
+    jp, tips, op, con, length = G.reward_plugin_inputs(case["index"])
+    dense = case["reward"] == "dense"
+    for e in range(case["E"]):
+        prev = None
+        for t in range(length[e]):
+            assert np.array_equal(oracle_finger_tips(jp[e, t]), tips[e, t])
+            out, prev = oracle_reward_compute(jp[e, t], tips[e, t], op[e, t], con[e, t], prev, (1.0, 0.5, 0.3, 0.2),
+                                              dense=dense)
+            assert math.isclose(out[0], z["reward"][e, t], rel_tol=1e-12, abs_tol=1e-15), (e, t)
+            np.testing.assert_allclose(out[1:], z["comps"][e, t], rtol=1e-12, atol=1e-15)

@@ -109,6 +109,15 @@ class SchedArgs(C.Structure):
                [("scratch_bytes", C.c_int64), ("summary", C.c_void_p)]
 
 
+class SchedPackedArgs(C.Structure):
+    _fields_ = [("packs", C.c_void_p), ("pack_words", C.c_int64), ("bits", C.c_int32), ("world", C.c_int32),
+                ("horizon", C.c_int32), ("num_envs", C.c_int64), ("window", C.c_int32),
+                ("max_candidates", C.c_int32), ("threshold", C.c_double), ("min_episodes", C.c_int64),
+                ("episodes_before", C.c_int64)] + \
+               [(k, C.c_void_p) for k in ("tail_in", "tail_len_in", "tail_out", "tail_len_out", "scratch")] + \
+               [("scratch_bytes", C.c_int64), ("summary", C.c_void_p), ("where", C.c_void_p)]
+
+
 SCHED_MAX_CANDIDATES = 64  # DXRL_SCHED_MAX_CANDIDATES
 
 
@@ -168,6 +177,12 @@ _SIGS = {
     "dxrl_evaluate": (C.c_int, [_P, C.POINTER(EvalArgs), _P]),
     "dxrl_sched_scratch_bytes": (C.c_int, [_I32, _I32, _I64, _I32, C.POINTER(_I64)]),
     "dxrl_sched_scan": (C.c_int, [_I32, C.POINTER(SchedArgs), _P]),
+    "dxrl_sched_pack_words": (C.c_int, [_I32, _I64, _I32, _I32, C.POINTER(_I64)]),
+    "dxrl_sched_pack": (C.c_int, [_I32, _P, _I32, _I64, _I32, _I32, _P, _P]),
+    "dxrl_sched_packed_scratch_bytes": (C.c_int, [_I32, _I32, _I64, _I32, C.POINTER(_I64)]),
+    "dxrl_sched_scan_packed": (C.c_int, [_I32, C.POINTER(SchedPackedArgs), _P]),
+    "dxrl_sched_candidate_steps": (C.c_int, [_I32, _P, _I32, _I64, _I32, _I32, _P, _P, _P, _P]),
+    "dxrl_sched_finish": (C.c_int, [_I32, _P, _P, _P]),
     "dxrl_pg_adam": (C.c_int, [_I32, _P, _P, _P, _P, _I64, _F64, _F64, _F64, _F64, _I64, _P, _F64, _P]),
     "dxrl_pg_optimizer_step": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P, _I64, _F64, _F64, _F64, _F64, _I64, _F64,
                                          _P, _P, _P, _P]),

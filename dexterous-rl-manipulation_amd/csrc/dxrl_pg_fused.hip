@@ -1233,16 +1233,12 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
         const char* v = getenv("DXRL_FUSED_TILE");
         return v && atoi(v) == 64 ? 64 : 128;
     }();
-    static const int waves128 = [] {
-        const char* v = getenv("DXRL_FUSED_WAVES");  // A/B for 128-sample tiles: 4 = one wave per SIMD
-        return v && atoi(v) == 4 ? 4 : 8;
-    }();
     static const int cus = [device] {
         int n = 0;
         return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0 ? n
                                                                                                             : 256;
     }();
-    const int waves = tile == 64 ? 4 : waves128;
+    const int waves = tile == 64 ? 4 : 8;  // the instantiations launched below (128-sample tiles: 8 waves)
     const int64_t ntiles = (a->rows + tile - 1) / tile;
     const int64_t cap = (int64_t)cus * (tile == 64 ? 2 : 1);
     int64_t g64 = a->grid < cap ? a->grid : cap;

@@ -314,8 +314,16 @@ class EpisodeProgram:
                 N.call("dxrl_evaluate", env.handle, C.byref(a), st.cuda_stream)
             e1.record(st)
         keep = (env, a, d_lane, d_seg, mean, d_pol, d_noise, d_reset, queue)  # alive until the stream is done
-        return _PendingRun(st, e0, e1, max(1, int(repeat)), status, plan.props, keep_history, trajectories,
-                           (out_ret, out_len, out_suc, out_con, out_hist, used, o_traj, a_traj), keep, E)
+        outs = (out_ret, out_len, out_suc, out_con, out_hist, used, o_traj, a_traj)
+        if st != torch.cuda.current_stream(dev):
+            # allocated on the current stream, used on `st`: the caching allocator must not hand
+            # these blocks out again before `st` has passed the launch, even if the _PendingRun
+            # is dropped without result()
+            for x in outs + (status, d_lane, d_seg, mean, d_pol, d_noise, d_reset, queue, env._slab_owner):
+                if isinstance(x, torch.Tensor):
+                    x.record_stream(st)
+        return _PendingRun(st, e0, e1, max(1, int(repeat)), status, plan.props, keep_history, trajectories, outs,
+                           keep, E)
 
 
     def run_facade(self, policy, trajectories: bool = False) -> EvalRecords:

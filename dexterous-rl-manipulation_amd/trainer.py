@@ -15,7 +15,8 @@ actor-critic with GAE and policy gradients on top of the same env.  One
   4. actor forward, PPO-clip / value / entropy heads (``dxrl_pg_heads``);
   5. backward GEMMs (input grads with fused tanh' gate, weight grads by
      split-K over samples with the bias as an extra ones-row);
-  6. one flat f32 gradient all-reduce over RCCL (world > 1);
+  6. the f32 gradient SUM all-reduce over RCCL (world > 1), in two halves on a side stream:
+     the critic's beside the actor's train pass, the actor's before Adam;
   7. global-norm clip + Adam on the f32 master, bf16 repack.
 
 Every matrix contraction runs in libdxrl.so; torch only owns the buffers.
@@ -81,6 +82,7 @@ class TrainerConfig:
     minibatches: int = 1                     # time-contiguous minibatches per epoch, order shuffled per epoch
                                              # (1 x 1: one update, ratio == 1 -- an A2C-style step)
     success_rule: str = "terminated"         # "training" (episode_utils.py:52) or "terminated"
+    overlap_comm: bool = True                # collectives on a side stream, overlapped with the train passes
 
 
 def minibatch_bounds(M: int, B: int, round_samples: int):
@@ -136,6 +138,14 @@ class PGTrainer:
         # collectives run with several ranks or with an explicit process group (a world-1 group
         # executes the same RCCL calls: bench.py --dist, tests/test_gpu_rccl.py)
         self.collective = process_group is not None or world_size > 1
+        # Exchanges that overlap compute (collective mode): the advantage-moment all-gather runs
+        # beside the critic's train pass (which does not read the normalisation), the critic
+        # half of the gradient all-reduce beside the actor's, the scheduler's code exchange
+        # beside critic values.  Element-wise the same SUMs, so results do not change.
+        self._comm = None
+        if self.collective and cfg.overlap_comm and env.device.type == "cuda":
+            self._comm = torch.cuda.Stream(device=env.device)
+        self._stats_pending = self._grads_pending = False
         self.global_M = global_count(self.M, self.world, self.pg)  # samples of all ranks per iteration
         if self.global_M != self.M * self.world:
             raise ValueError(f"every rank needs the same num_envs * horizon ({self.M} here, {self.global_M} over "
@@ -313,12 +323,19 @@ class PGTrainer:
     def actor_train(self):
         start, rows = self._mb
         self._loss_rows = rows
+        if self._stats_pending:  # the actor's head normalises the advantages with the global moments
+            torch.cuda.current_stream(self.dev).wait_stream(self._comm)
+            self._stats_pending = False
         N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(0, True, rows, start)), self._s())
 
     def critic_train(self):
         start, rows = self._mb
         self._loss_rows = rows
         N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(1, True, rows, start)), self._s())
+        if self._comm is not None:  # the critic half's SUM all-reduce runs beside the actor's pass
+            with self._on_comm():
+                self._allreduce(self.grads[OFF["W1c"]:])
+            self._grads_pending = True
 
     def ppo_updates(self):
         """epochs x minibatches PPO-clip updates (actor + critic pass and an Adam step each)
@@ -330,8 +347,8 @@ class PGTrainer:
         for _ in range(c.epochs):
             for k in rng.permutation(c.minibatches):
                 self._mb = (bounds[k], bounds[k + 1] - bounds[k])
-                self.actor_train()
                 self.critic_train()
+                self.actor_train()
                 self.optimizer_step()
         self._mb = (0, self.M)
 
@@ -343,7 +360,8 @@ class PGTrainer:
         if self.cfg.fused and self.cfg.epochs * self.cfg.minibatches > 1:
             ph = ["rollout", "critic_values", "advantages", "ppo_updates"]
         elif self.cfg.fused:
-            ph = ["rollout", "critic_values", "advantages", "actor_train", "critic_train", "optimizer_step"]
+            # the critic first: its pass does not need the (all-gathered) normalisation moments
+            ph = ["rollout", "critic_values", "advantages", "critic_train", "actor_train", "optimizer_step"]
         else:
             ph = ["rollout", "critic_forward", "advantages", "actor_forward", "heads", "backward", "optimizer_step"]
         if self.scheduler is not None:  # feed launched behind the rollout, applied after the learner
@@ -360,9 +378,25 @@ class PGTrainer:
         # every rank's (count, mean, M2) in rank order, merged on device (identical on all ranks);
         # one rank: dxrl_pg_gae already wrote the combined statistics
         if self.collective:
-            gather_adv_moments_(self.moments_all, self.stats, self.world, self.pg)
-            N.call("dxrl_pg_adv_combine", self.dev.index, N.ptr(self.moments_all), self.world, N.ptr(self.stats),
-                   self._s())
+            with self._on_comm():
+                gather_adv_moments_(self.moments_all, self.stats, self.world, self.pg)
+                N.call("dxrl_pg_adv_combine", self.dev.index, N.ptr(self.moments_all), self.world,
+                       N.ptr(self.stats), self._s())
+            self._stats_pending = self._comm is not None
+
+    def _on_comm(self):
+        """Context for an exchange: the comm stream (after everything enqueued so far on the
+        compute stream), or the compute stream itself without overlap."""
+        if self._comm is None:
+            return _null()
+        self._comm.wait_stream(torch.cuda.current_stream(self.dev))
+        return torch.cuda.stream(self._comm)
+
+    def _join_comm(self):
+        """The compute stream waits for every exchange issued so far."""
+        if self._comm is not None:
+            torch.cuda.current_stream(self.dev).wait_stream(self._comm)
+        self._stats_pending = self._grads_pending = False
 
     def heads(self):
         c, p = self.cfg, N.ptr
@@ -390,7 +424,11 @@ class PGTrainer:
         + one clipped-Adam-and-pack launch writing the next master / moments into the spare
         buffers, which then become current (params / m1 / m2 are swapped, not copied)."""
         c = self.cfg
-        self._allreduce(self.grads)
+        if self._grads_pending:  # critic half already in flight on the comm stream
+            self._allreduce(self.grads[:OFF["W1c"]])
+            self._join_comm()
+        else:
+            self._allreduce(self.grads)
         self.step_count += 1
         if self._spare is None:
             self._spare = tuple(torch.empty_like(t) for t in (self.params, self.m1, self.m2))
@@ -409,18 +447,20 @@ class PGTrainer:
         progression pushes the new config into the device table (effective at each env's next
         reset, as component_ablation.py:165-166 swaps it between episodes).
 
-        The rollout writes one u16 episode-end code per (step, env); ranks all-gather them
-        (RCCL) and dxrl_sched_scan walks them on the device.  With history="window" and the
-        base success-window rule only a few numbers cross PCIe (apply_device_summary);
-        otherwise (history="full", StepBasedScheduler, > 64 pending progressions) the codes
-        are copied to the host and fed through update_batch.  Either way every rank's
+        The rollout writes one u16 episode-end code per (step, env) and dxrl_sched_scan walks
+        them on the device.  With history="window" and the base success-window rule only a few
+        numbers cross PCIe (apply_device_summary); sharded, the ranks exchange compact packs
+        instead of their codes (dxrl_sched_pack: per-step sums, the rank's last `window` codes,
+        and one success bit per episode only while progressions remain;
+        dxrl_sched_scan_packed + one all-reduce of <= 64 candidate step counts).  Otherwise
+        (history="full", StepBasedScheduler, > 64 pending progressions) every rank's codes are
+        all-gathered, copied to the host and fed through update_batch.  Either way every rank's
         scheduler sees the same global stream, so all ranks progress together."""
         self.scheduler = scheduler
         self.env.set_curriculum(scheduler.get_current_config())
         d, n, T = self.dev, self.n, self.T
         self.ep_code = torch.zeros(T * n, dtype=torch.int16, device=d)
-        self.codes_all = self.ep_code if not self.collective else torch.zeros(self.world * T * n, dtype=torch.int16,
-                                                                              device=d)
+        self.codes_all = self.ep_code if not self.collective else None  # host mode's all-gather (lazy)
         w = max(1, int(scheduler.window_size))
         self._sched_w = w
         self._tail_dev = torch.zeros(2, w, dtype=torch.int16, device=d)
@@ -428,7 +468,20 @@ class PGTrainer:
         self._tail_in_host = torch.zeros(w, dtype=torch.int16).pin_memory()
         self._tail_len_host = torch.zeros(1, dtype=torch.int32).pin_memory()
         nb = C.c_int64()
-        N.call("dxrl_sched_scratch_bytes", self.world, T, n, w, C.byref(nb))
+        # sharded: the packed exchange (dxrl_sched_pack holds a step's episode steps in u32)
+        self._packed = self.collective and n < (1 << 18)
+        if self._packed:
+            import torch.distributed as dist
+            self.rank = dist.get_rank(self.pg) if self.pg is not None else dist.get_rank()
+            wb = C.c_int64()
+            N.call("dxrl_sched_pack_words", T, n, w, 1, C.byref(wb))
+            self._pack = torch.zeros(wb.value, dtype=torch.int32, device=d)
+            self._packs_all = torch.zeros(self.world * wb.value, dtype=torch.int32, device=d)
+            self._where = torch.zeros(N.SCHED_MAX_CANDIDATES, 3, dtype=torch.int32, device=d)
+            self._cand_steps = torch.zeros(N.SCHED_MAX_CANDIDATES, dtype=torch.int64, device=d)
+            N.call("dxrl_sched_packed_scratch_bytes", self.world, T, n, w, C.byref(nb))
+        else:
+            N.call("dxrl_sched_scratch_bytes", 1, T, n, w, C.byref(nb))
         self._sched_scratch = torch.empty(nb.value, dtype=torch.uint8, device=d)
         self._summary = torch.zeros(4 + 3 * N.SCHED_MAX_CANDIDATES, dtype=torch.int64, device=d)
         self._summary_host = torch.zeros_like(self._summary, device="cpu").pin_memory()
@@ -440,10 +493,16 @@ class PGTrainer:
     def schedule_feed(self):
         """Behind the rollout: all-gather the episode-end codes, scan them on the device and
         start the (tiny) summary copy; schedule_apply() consumes it after the learner."""
+        with self._on_comm():  # beside critic values (collective mode)
+            self._schedule_feed()
+
+    def _schedule_feed(self):
         sc = self.scheduler
-        all_gather_into_(self.codes_all, self.ep_code, self.world, self.pg)
         P = sc.remaining_progressions(N.SCHED_MAX_CANDIDATES)
-        if sc.history == "window" and sc._uses_success_window_rule() and P <= N.SCHED_MAX_CANDIDATES:
+        device = sc.history == "window" and sc._uses_success_window_rule() and P <= N.SCHED_MAX_CANDIDATES
+        if device and self.collective and not self._packed:
+            device = False  # the full-codes exchange below (very large shards)
+        if device:
             w = self._sched_w
             # the host lists are authoritative for the window carried in (success bits are all
             # the scan reads); pinned staging, so the copies queue behind the rollout without a
@@ -454,24 +513,52 @@ class PGTrainer:
                 self._tail_in_host[:len(tail)] = torch.tensor(tail, dtype=torch.int16)
             self._tail_dev[0].copy_(self._tail_in_host, non_blocking=True)
             self._tail_len_dev[0:1].copy_(self._tail_len_host, non_blocking=True)
-            a = N.SchedArgs()
-            a.codes, a.world, a.horizon, a.num_envs = N.ptr(self.codes_all), self.world, self.T, self.n
+            a = N.SchedPackedArgs() if self.collective else N.SchedArgs()
             a.window, a.max_candidates, a.threshold = w, P, float(sc.success_rate_threshold)
             a.min_episodes, a.episodes_before = int(sc.min_episodes_before_progression), int(sc.total_episodes)
             a.tail_in, a.tail_len_in = N.ptr(self._tail_dev[0]), N.ptr(self._tail_len_dev[0:1])
             a.tail_out, a.tail_len_out = N.ptr(self._tail_dev[1]), N.ptr(self._tail_len_dev[1:2])
             a.scratch, a.scratch_bytes, a.summary = N.ptr(self._sched_scratch), self._sched_scratch.numel(), \
                 N.ptr(self._summary)
-            N.call("dxrl_sched_scan", self.dev.index, C.byref(a), self._s())
+            a.world, a.horizon, a.num_envs = self.world, self.T, self.n
+            if not self.collective:  # one rank, no exchange: scan the codes themselves
+                a.codes = N.ptr(self.ep_code)
+                N.call("dxrl_sched_scan", self.dev.index, C.byref(a), self._s())
+            else:
+                self._packed_feed(a, P)
             self._summary_host.copy_(self._summary, non_blocking=True)
             self._tail_out_host.copy_(self._tail_dev[1], non_blocking=True)
             self._sched_mode = "device"
         else:
+            if self.codes_all is None:
+                self.codes_all = torch.zeros(self.world * self.T * self.n, dtype=torch.int16, device=self.dev)
+            all_gather_into_(self.codes_all, self.ep_code, self.world, self.pg)
             if self._codes_host is None:
                 self._codes_host = torch.zeros(self.codes_all.numel(), dtype=torch.int16).pin_memory()
             self._codes_host.copy_(self.codes_all, non_blocking=True)
             self._sched_mode = "host"
-        self._sched_event.record(torch.cuda.current_stream(self.dev))
+        self._sched_event.record(torch.cuda.current_stream(self.dev))  # the comm stream in collective mode
+
+    def _packed_feed(self, a, P):
+        """Sharded device feed: pack -> all-gather the packs -> scan them -> (candidates) the
+        owners' in-block step counts, SUM over ranks -> finished summary.  The success bits
+        travel only while progressions are still possible (P > 0)."""
+        bits = 1 if P > 0 else 0
+        wd = C.c_int64()
+        N.call("dxrl_sched_pack_words", self.T, self.n, self._sched_w, bits, C.byref(wd))
+        W = wd.value
+        pack, packs = self._pack[:W], self._packs_all[:self.world * W]
+        s = self._s()
+        N.call("dxrl_sched_pack", self.dev.index, N.ptr(self.ep_code), self.T, self.n, self._sched_w, bits,
+               N.ptr(pack), s)
+        all_gather_into_(packs, pack, self.world, self.pg)
+        a.packs, a.pack_words, a.bits, a.where = N.ptr(packs), W, bits, N.ptr(self._where)
+        N.call("dxrl_sched_scan_packed", self.dev.index, C.byref(a), s)
+        if P > 0:
+            N.call("dxrl_sched_candidate_steps", self.dev.index, N.ptr(self.ep_code), self.T, self.n, self.rank, P,
+                   N.ptr(self._where), N.ptr(self._summary), N.ptr(self._cand_steps), s)
+            all_reduce_sum_(self._cand_steps[:P], self.world, self.pg)
+            N.call("dxrl_sched_finish", self.dev.index, N.ptr(self._cand_steps), N.ptr(self._summary), s)
 
     def schedule_apply(self):
         """Replay the iteration's episodes into the scheduler; push a progression to the env."""
@@ -510,8 +597,8 @@ class PGTrainer:
         for name in self.phases():
             with profiling.range_(f"pg.{name}") if marks else _null():
                 if name == "ppo_updates" and not update:
-                    self.actor_train()
                     self.critic_train()
+                    self.actor_train()
                 elif name != "optimizer_step" or update:
                     getattr(self, name)()
         self.iteration_index += 1

@@ -363,6 +363,47 @@ typedef struct dxrl_sched_args {
 int dxrl_sched_scratch_bytes(int32_t world, int32_t horizon, int64_t num_envs, int32_t window, int64_t* bytes);
 int dxrl_sched_scan(int32_t device, const dxrl_sched_args* args, void* stream);
 
+/* The same feed with a compacted exchange between ranks (what a sharded run all-gathers instead
+ * of the world x T x N codes).  Each rank packs its own codes [T][N]:
+ *   header (episodes, tail length), per-step (episodes, steps, successes), its last `window`
+ *   codes, and -- only while progressions are still possible (bits = 1) -- one success bit
+ *   per episode;
+ * = 4 (2 + 3 T + window / 2) bytes, + T N / 8 with bits.  The ranks all-gather the packs,
+ * dxrl_sched_scan_packed walks them in (end step, global env id) order exactly as
+ * dxrl_sched_scan walks the codes, and reports every candidate's steps only through the start
+ * of its (step, rank) block plus where it lies (`where`); the owning rank adds the steps inside
+ * the block (dxrl_sched_candidate_steps -> i64 [P], zero for others), the ranks SUM those P
+ * values (all-reduce) and dxrl_sched_finish adds them into the summary.  The summary / tail
+ * equal dxrl_sched_scan's on the all-gathered codes. */
+int dxrl_sched_pack_words(int32_t horizon, int64_t num_envs, int32_t window, int32_t bits, int64_t* words);
+int dxrl_sched_pack(int32_t device, const uint16_t* codes, int32_t horizon, int64_t num_envs, int32_t window,
+                    int32_t bits, uint32_t* pack, void* stream);
+typedef struct dxrl_sched_packed_args {
+    const void* packs;         /* u32 [world][pack_words] all-gathered packs, rank order  */
+    int64_t pack_words;        /* dxrl_sched_pack_words(horizon, num_envs, window, bits)  */
+    int32_t bits;              /* the packs carry success bits (needed when max_candidates > 0) */
+    int32_t world, horizon;
+    int64_t num_envs;          /* N per rank                                              */
+    int32_t window, max_candidates;
+    double threshold;
+    int64_t min_episodes, episodes_before;
+    const uint16_t* tail_in;   /* as dxrl_sched_args                                      */
+    const int32_t* tail_len_in;
+    uint16_t* tail_out;
+    int32_t* tail_len_out;
+    void* scratch;             /* dxrl_sched_packed_scratch_bytes()                       */
+    int64_t scratch_bytes;
+    int64_t* summary;          /* as dxrl_sched_args (candidate steps: block prefix until finished) */
+    int32_t* where;            /* i32 [P][3] per candidate: owning rank, end step, index in its block */
+} dxrl_sched_packed_args;
+int dxrl_sched_packed_scratch_bytes(int32_t world, int32_t horizon, int64_t num_envs, int32_t window,
+                                    int64_t* bytes);
+int dxrl_sched_scan_packed(int32_t device, const dxrl_sched_packed_args* args, void* stream);
+int dxrl_sched_candidate_steps(int32_t device, const uint16_t* codes, int32_t horizon, int64_t num_envs,
+                               int32_t rank, int32_t max_candidates, const int32_t* where, const int64_t* summary,
+                               int64_t* partial, void* stream);
+int dxrl_sched_finish(int32_t device, const int64_t* partial, int64_t* summary, void* stream);
+
 typedef struct dxrl_pg_heads_args {
     const float* mu;           /* f32 [M][32] actor head output            */
     const float* values;       /* f32 [M] critic value                     */

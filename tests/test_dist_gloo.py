@@ -11,7 +11,8 @@ what PGTrainer exchanges, through the functions PGTrainer itself calls
     k_stats_combine);
   * global_count + loss_scales -> the per-sample 1/(global samples) scale and the
     per-rank ent_coef/world the kernels receive (ragged shards included);
-  * one SUM all-reduce of the flat gradient buffer.
+  * the SUM all-reduce of the flat gradient buffer, also in the trainer's two-halves form
+    (the critic half overlapped with the actor's train pass) == one all-reduce.
 """
 import os
 import socket
@@ -68,7 +69,17 @@ def _worker(rank, world, port, out):
     scales = D.loss_scales(D.global_count(nl * T, topo.world, topo.group), world, CFG["ent_coef"])
     g, info = R.loss_and_grads(params, o, a, lp, rw, dn, nl, T, CFG, bf16=False, norm_stats=norm_stats,
                                scales=scales)
+    # the trainer's overlapped form: the critic half (the tail of the buffer) reduced on its own,
+    # then the actor half -- element-wise the same SUM as one all-reduce of the whole buffer
+    gs = g.clone()
+    cut = gs.numel() // 3
+    D.all_reduce_sum_(gs[cut:], topo.world, topo.group)
+    D.all_reduce_sum_(gs[:cut], topo.world, topo.group)
     D.all_reduce_sum_(g, topo.world, topo.group)
+    if world == 2:
+        assert torch.equal(gs, g)  # a + b: no order to differ in
+    else:
+        assert torch.allclose(gs, g, rtol=1e-12, atol=1e-15)
     # the global moments are those of the concatenated batch
     adv_full = full_info["adv"].double()
     assert seen["moments"][0] == n * T

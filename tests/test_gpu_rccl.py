@@ -6,7 +6,8 @@ advantage-moment triple, the all-gather of the u16 episode codes as bytes, the i
 global_count SUM and the f64 MAX.  Each must return its input; and a PGTrainer driven
 through that group (3 full iterations, curriculum-scheduler and fused-noise configs) must
 give the group-less trainer's gradients, statistics, episode codes and parameters bit for
-bit.  Multi-rank semantics are covered by tests/test_dist_gloo.py (CPU) and
+bit -- with its exchanges on the side stream overlapping the train passes (the default) and
+serialised on the compute stream (overlap_comm=False).  Multi-rank semantics are covered by tests/test_dist_gloo.py (CPU) and
 tests/test_gpu_dist.py (two ranks on one GPU over gloo)."""
 import os
 import socket
@@ -36,12 +37,14 @@ def test_rccl_world1_collectives_and_trainer(tmp_path):
     assert res["allreduce_equal"] and res["moments_equal"] and res["codes_equal"]
     assert res["global_count"] == 12345 and res["max"] == 3.25
     for config in ("default", "variable"):
-        a, b = res[config]
-        assert a["collective"] and not b["collective"]
-        for k in ("grads", "stats", "codes"):
-            assert len(a[k]) == len(b[k])
-            for x, y in zip(a[k], b[k]):
-                assert torch.equal(x, y), (config, k)
-        assert torch.equal(a["params"], b["params"]), config
-        if config == "default":
-            assert a["sched"] == b["sched"]
+        a, b, c = res[config]
+        assert a["collective"] and not b["collective"] and c["collective"]
+        assert a["overlapped"] and not c["overlapped"]
+        for other in (b, c):
+            for k in ("grads", "stats", "codes"):
+                assert len(a[k]) == len(other[k])
+                for x, y in zip(a[k], other[k]):
+                    assert torch.equal(x, y), (config, k)
+            assert torch.equal(a["params"], other["params"]), config
+            if config == "default":
+                assert a["sched"] == other["sched"]

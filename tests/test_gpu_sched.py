@@ -100,3 +100,88 @@ def test_trainer_device_feed_equals_host_feed(threshold):
         assert ma == "device" and mb == "host"
         assert a == b and sa == sb
     assert runs[0][-1][0]["num_progressions"] > 0
+
+
+def _scan_packed(N, codes, window, thr, min_ep, before, P, tail, bits=None):
+    """The compacted exchange with `world` ranks simulated on one GPU: every rank packs its own
+    codes (dxrl_sched_pack), the packs are concatenated in rank order (what the all-gather
+    produces), every rank would run dxrl_sched_scan_packed (once here), each rank's
+    dxrl_sched_candidate_steps partials are summed (the all-reduce) and dxrl_sched_finish
+    completes the summary."""
+    world, T, n = codes.shape
+    dev = torch.device("cuda", 0)
+    bits = int(P > 0) if bits is None else bits
+    words = C.c_int64()
+    N.call("dxrl_sched_pack_words", T, n, window, bits, C.byref(words))
+    W = words.value
+    assert W == 2 + 3 * T + (window + 1) // 2 + (((T * n + 31) // 32) if bits else 0)
+    packs = torch.full((world, W), 0x7EADBEEF, dtype=torch.int32, device=dev)
+    own = []
+    for r in range(world):
+        c = torch.from_numpy(np.ascontiguousarray(codes[r]).astype(np.uint16).view(np.int16)).to(dev)
+        own.append(c)
+        N.call("dxrl_sched_pack", 0, N.ptr(c), T, n, window, bits, N.ptr(packs[r]), N.stream_of(dev))
+    tail_in = torch.zeros(window, dtype=torch.int16, device=dev)
+    tail_in[:len(tail)] = torch.tensor(np.asarray(tail, dtype=np.int64).astype(np.uint16).view(np.int16))
+    tail_out = torch.full((window,), -1, dtype=torch.int16, device=dev)
+    tl = torch.tensor([len(tail), -1], dtype=torch.int32, device=dev)
+    nb = C.c_int64()
+    N.call("dxrl_sched_packed_scratch_bytes", world, T, n, window, C.byref(nb))
+    scratch = torch.empty(nb.value, dtype=torch.uint8, device=dev)
+    summary = torch.full((4 + 3 * N.SCHED_MAX_CANDIDATES,), -7, dtype=torch.int64, device=dev)
+    where = torch.full((N.SCHED_MAX_CANDIDATES, 3), -1, dtype=torch.int32, device=dev)
+    a = N.SchedPackedArgs()
+    a.packs, a.pack_words, a.bits, a.world, a.horizon, a.num_envs = N.ptr(packs), W, bits, world, T, n
+    a.window, a.max_candidates, a.threshold, a.min_episodes, a.episodes_before = window, P, thr, min_ep, before
+    a.tail_in, a.tail_len_in, a.tail_out, a.tail_len_out = N.ptr(tail_in), N.ptr(tl[0:1]), N.ptr(tail_out), \
+        N.ptr(tl[1:2])
+    a.scratch, a.scratch_bytes, a.summary, a.where = N.ptr(scratch), nb.value, N.ptr(summary), N.ptr(where)
+    N.call("dxrl_sched_scan_packed", 0, C.byref(a), N.stream_of(dev))
+    if P > 0:
+        parts = torch.zeros(world, N.SCHED_MAX_CANDIDATES, dtype=torch.int64, device=dev)
+        for r in range(world):
+            N.call("dxrl_sched_candidate_steps", 0, N.ptr(own[r]), T, n, r, P, N.ptr(where), N.ptr(summary),
+                   N.ptr(parts[r]), N.stream_of(dev))
+        total = parts.sum(0)
+        N.call("dxrl_sched_finish", 0, N.ptr(total), N.ptr(summary), N.stream_of(dev))
+    torch.cuda.synchronize()
+    s = summary.cpu().numpy()
+    nl = int(tl[1].item())
+    return s, tail_out.cpu().numpy().view(np.uint16)[:nl].astype(np.int64), W
+
+
+@pytest.mark.parametrize("world,T,n", [(1, 7, 5), (2, 13, 33), (3, 4, 100), (2, 200, 4096), (8, 20, 1000),
+                                       (8, 3, 2500), (5, 9, 1)])
+def test_packed_exchange_matches_restatement(N, world, T, n):
+    """The compacted C3 exchange (per-rank packs: step summaries, own tail, success bits only
+    while progressions remain) gives dxrl_sched_scan's summary and tail -- checked against the
+    NumPy restatement -- on random multi-rank tapes, sparse and dense episode ends, with and
+    without candidates."""
+    rng = np.random.default_rng(world * 7919 + T * 31 + n)
+    for trial in range(6):
+        p_end, p_succ = rng.random(), rng.random()
+        if trial == 0:
+            p_end = 1.0  # every env-step ends an episode (config_easy)
+        lens = rng.integers(1, 16383, (world, T, n))
+        codes = np.where(rng.random((world, T, n)) < p_end, (lens << 1) | (rng.random((world, T, n)) < p_succ), 0)
+        window = int(rng.choice([1, 2, 15, 20, 64, 1000]))
+        thr = float(rng.choice([0.0, 0.3, 0.5, 0.9, 1.0]))
+        min_ep, before = int(rng.integers(0, 50)), int(rng.integers(0, 3000))
+        P = int(rng.integers(0, N.SCHED_MAX_CANDIDATES + 1)) if trial % 2 else 0
+        tail = (rng.random(min(window, before)) < p_succ).astype(np.int64)
+        s, new_tail, W = _scan_packed(N, codes, window, thr, min_ep, before, P, tail)
+        r = SR.scan(codes, window, thr, min_ep, before, P, tail)
+        assert (s[0], s[1], s[2]) == (r["episodes"], r["steps"], r["successes"]), trial
+        found = int(s[3])
+        assert found == len(r["candidates"]), (trial, found, len(r["candidates"]))
+        assert [tuple(int(x) for x in s[4 + 3 * j:7 + 3 * j]) for j in range(found)] == r["candidates"], trial
+        assert np.array_equal(new_tail, r["tail"]), trial
+        if P == 0:  # steady state: the exchange does not grow with the envs at all
+            assert W == 2 + 3 * T + (window + 1) // 2
+
+
+def test_packed_exchange_empty_batch(N):
+    codes = np.zeros((3, 5, 9), dtype=np.int64)
+    for P in (0, 3):
+        s, tail, _ = _scan_packed(N, codes, 4, 0.5, 0, 10, P, [1, 0, 1, 1])
+        assert list(s[:4]) == [0, 0, 0, 0] and list(tail) == [1, 0, 1, 1]

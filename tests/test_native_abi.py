@@ -73,7 +73,7 @@ def test_gae_partial_size_query(native):
 
 STRUCTS = ["dxrl_curriculum", "dxrl_env_config", "dxrl_env_layout", "dxrl_learner_layout", "dxrl_learner_config",
            "dxrl_rollout_io", "dxrl_pg_rollout_args", "dxrl_pg_heads_args",
-           "dxrl_pg_fused_args", "dxrl_eval_segment", "dxrl_eval_args", "dxrl_sched_args"]
+           "dxrl_pg_fused_args", "dxrl_eval_segment", "dxrl_eval_args", "dxrl_sched_args", "dxrl_sched_packed_args"]
 
 
 def test_ctypes_struct_layouts_match_c(native):
@@ -82,7 +82,8 @@ def test_ctypes_struct_layouts_match_c(native):
               "dxrl_learner_config": native.LearnerConfig, "dxrl_rollout_io": native.RolloutIO,
               "dxrl_pg_rollout_args": native.PgRolloutArgs, "dxrl_pg_heads_args": native.PgHeadsArgs,
               "dxrl_pg_fused_args": native.PgFusedArgs, "dxrl_eval_segment": native.EvalSegment,
-              "dxrl_eval_args": native.EvalArgs, "dxrl_sched_args": native.SchedArgs}
+              "dxrl_eval_args": native.EvalArgs, "dxrl_sched_args": native.SchedArgs,
+              "dxrl_sched_packed_args": native.SchedPackedArgs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for s in STRUCTS:
         lines.append(f'printf("{s} %zu\\n", sizeof({s}));')

@@ -30,4 +30,4 @@ for nm in names:
     b.record()
     torch.cuda.synchronize()
     out[nm] = round(a.elapsed_time(b) / reps, 4)
-print(os.environ.get("DXRL_FUSED_WAVES", "4"), out, tr.loss_stats())
+print(os.environ.get("DXRL_FUSED_TILE", "128"), out, tr.loss_stats())

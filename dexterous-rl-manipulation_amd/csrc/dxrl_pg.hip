@@ -894,11 +894,12 @@ __device__ __forceinline__ void lds_barrier() {
 // One env lane's draws, computed by its aux twin (structure of arrays over the 256 env lanes):
 // the action / dynamics noise normals and the reset uniforms (at the env's exact reset counter)
 // of the current step, and the observation-noise normals of the lane's obs elements
-// (row_obs_elem) for the next observation row.  Single-buffered: each is written in the head
-// phase and read before the next head phase.  The reward inputs (WsReward) are double-buffered
+// (row_obs_elem) for the next observation row.  The step's draws are single-buffered (written in
+// the head phase, read before the next head phase); the observation noise is double-buffered by
+// row parity (row t + 1's is written in step t's P0 while the env lanes read row t's).  The reward inputs (WsReward) are double-buffered
 // by step parity: the env lanes write step t's while the aux lanes settle step t-1's.
 struct WsDraws {
-    float eps[256], dzn[256], on[4][256];
+    float eps[256], dzn[256], on[2][4][256];  // on: double-buffered by observation row parity
     double u1[256], u2[256];
 };
 struct WsSampler {     // one env lane's extra reset draw: has ? lo + span u : cst
@@ -915,13 +916,13 @@ struct WsReward {      // an env's dense-reward inputs and episode end of one st
 };
 
 // Step t of a workgroup (16 envs, 8 waves):
-//   P0  env lanes write the observation row (+ observation noise drawn in step t-1's P3)
+//   P0  env lanes write the observation row (+ its observation noise, drawn in step t-1's P0);
+//       aux lanes meanwhile draw the next row's observation noise (other parity buffer)
 //   P1  all waves: L1, one 32-column tile each            (the env lanes also store the obs row)
 //   P2  all waves: L2, one 32-column tile each
 //   P3  env wave 3: the mu head; all env waves: the object update (env_object_step).  In their
 //       shadow, one drawing aux wave per SIMD (step_draws): wave 4 step t's action noise, waves
-//       5, 6, 7 the reset uniforms at each env's exact counter (step t-1's episode end is known);
-//       aux lanes: step t+1's observation noise
+//       5, 6, 7 the reset uniforms at each env's exact counter (step t-1's episode end is known)
 //   P4  env lanes: a = mu + sigma eps, dynamics, contacts, termination, auto-reset.
 //       Aux lanes: the same a, log pi (DPP row sum in action order), the act / log pi tape, then
 //       settle step t-1's reward and episode bookkeeping
@@ -1142,7 +1143,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             else if (k < kReset) DR.u2[16 * e + k - kD] = u;
         }
     };
-    const auto obs_draws = [&](uint64_t ctr) {  // the observation noise of row ctr
+    const auto obs_draws = [&](uint64_t ctr, int buf) {  // the observation noise of row ctr -> DR.on[buf]
         if (obs_noise && s < (kObs + 3) / 4) {
             float nz[4];
             normals4(ctr, kStreamObs, s, nz);
@@ -1152,7 +1153,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
                 if (k < kObs) {
                     int ln, j;
                     obs_slot(k, ln, j);
-                    DR.on[j][rbase + ln] = nz[h];
+                    DR.on[buf][j][rbase + ln] = nz[h];
                 }
             }
             if (kDiag && p.obs_noise_tape) {  // parity tape: the value write_obs_row adds (row ctr - iteration T)
@@ -1205,10 +1206,10 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     // identity quaternion (ME:164) / finger contact, object velocity -- the values selected
     // without divergent branches, then at most four predicated 2-byte stores (the if / else-if
     // chain compiled to a serial walk of exec-masked regions on the env waves' critical path)
-    const auto write_obs_row = [&]() {
+    const auto write_obs_row = [&](int buf) {  // buf: the row's noise buffer (row parity)
         bf16* xr = X + eg * kXs;
         const auto put = [&](int j, float v, int k) {
-            if (obs_noise) v = v + p.obs_noise * DR.on[j][et_tid];
+            if (obs_noise) v = v + p.obs_noise * DR.on[buf][j][et_tid];
             xr[k] = to_bf16(v);
         };
         const float v2 = s < 3 ? (float)opd : (s < 7 ? (s == 3 ? 1.0f : 0.0f) : (float)((flags >> ((s - 7) & 31)) & 1u));
@@ -1357,13 +1358,16 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             st_last = t_;                                                                        \
         }                                                                                        \
     } while (0)
-    if (aux && live) obs_draws(p.iteration * (uint64_t)T);
+    if (aux && live) obs_draws(p.iteration * (uint64_t)T, 0);
     __syncthreads();
     WS_STAMP(7);
     for (int64_t t = 0; t < T; ++t) {
         const int64_t m = t * n + i;
         const uint64_t ctr = p.iteration * (uint64_t)T + (uint64_t)t;
-        if (!aux && live) write_obs_row();
+        if (!aux && live) write_obs_row((int)(t & 1));
+        // the next observation row's noise (aux lanes, own rows; counter-only, so drawn here where
+        // the aux waves wait for the env lanes' row, not in the head phase beside the draws)
+        if (aux && live && (!kDiag || !(p.diag & 256))) obs_draws(ctr + 1, (int)((t + 1) & 1));
         WS_STAMP(0);
         lds_barrier();
         if (!aux && live) tape_obs_row(m);
@@ -1399,10 +1403,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             for (int q = 0; q < 4; ++q) MU[(4 * g16 + q) * (kOut + 1) + r16] = acc[q] + b3_reg;
         }
         if (!kDiag || !(p.diag & 256)) {
-            // this step's draws (RW[(t - 1) & 1].rctr: the counters after step t-1's resets), the next
-            // observation row's noise (aux lanes, own rows)
+            // this step's draws (RW[(t - 1) & 1].rctr: the counters after step t-1's resets)
             if (aux) step_draws(ctr, t);
-            if (aux && live) obs_draws(ctr + 1);
         }
         WS_STAMP(3);
         lds_barrier();
@@ -1438,7 +1440,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     }
     if (live && !aux) {
         // bootstrap observation (slot T), then the state back to the slab
-        write_obs_row();
+        write_obs_row((int)(T & 1));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         tape_obs_row(T * n + i);

@@ -243,7 +243,12 @@ __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfr
 // W[n0 + 16 j + (l & 15)][32 k + 8 (l >> 4) ..+7].  Activation fragments stream through a ring
 // kD k-steps ahead (pinned by scheduling barriers).  bias_v[4 j + q]: the bias of column
 // n0 + 16 j + 4 (l >> 4) + q (or null: none).
-template <int KS, int NT, typename WF>
+// kSwzA / kSwzOut: the activation rows A / out are 256-element rows stored with their 16-byte
+// chunks XOR-swizzled by the row (chunk c of row r at chunk c ^ r, r < 16; swz16): the fragment
+// reads (ds_read_b128, lane groups of 16) are then conflict-free and the 8-byte epilogue stores
+// stay 2-way, where the padded 264-element pitch made every fragment read 2-way.
+__device__ __forceinline__ int swz16(int r, int col) { return ((((col >> 3) ^ r) << 3) | (col & 7)); }
+template <int KS, int NT, bool kSwzA = false, bool kSwzOut = false, typename WF>
 __device__ __forceinline__ void wave_layer16(const bf16* A, int lda, const WF& wfrag, int n0, bf16* out, int ldo,
                                              int lane, const float* bias_v = nullptr) {
     const int r = lane & 15, g = lane >> 4;
@@ -251,15 +256,19 @@ __device__ __forceinline__ void wave_layer16(const bf16* A, int lda, const WF& w
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     constexpr int kD = KS < 4 ? KS : 4;
+    const auto afrag = [&](int k) {
+        const int col = 32 * k + 8 * g;
+        return *reinterpret_cast<const bf16x8*>(A + r * lda + (kSwzA ? swz16(r, col) : col));
+    };
     bf16x8 a[kD];
 #pragma unroll
-    for (int k = 0; k < kD; ++k) a[k] = *reinterpret_cast<const bf16x8*>(A + r * lda + 32 * k + 8 * g);
+    for (int k = 0; k < kD; ++k) a[k] = afrag(k);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[j] = mfma16(wfrag(j, k), a[k % kD], acc[j]);
-        if (k + kD < KS) a[k % kD] = *reinterpret_cast<const bf16x8*>(A + r * lda + 32 * (k + kD) + 8 * g);
+        if (k + kD < KS) a[k % kD] = afrag(k + kD);
         __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
@@ -273,7 +282,8 @@ __device__ __forceinline__ void wave_layer16(const bf16* A, int lda, const WF& w
             v[q] = to_bf16(t.x);
             v[q + 1] = to_bf16(t.y);
         }
-        *reinterpret_cast<bf16x4*>(out + r * ldo + n0 + 16 * j + 4 * g) = v;
+        const int col = n0 + 16 * j + 4 * g;
+        *reinterpret_cast<bf16x4*>(out + r * ldo + (kSwzOut ? swz16(r, col) : col)) = v;
     }
 }
 
@@ -917,7 +927,8 @@ struct WsReward {      // an env's dense-reward inputs and episode end of one st
 
 // Step t of a workgroup (16 envs, 8 waves):
 //   P0  env lanes write the observation row (+ its observation noise, drawn in step t-1's P0);
-//       aux lanes meanwhile draw the next row's observation noise (other parity buffer)
+//       aux lanes meanwhile draw the next row's observation noise (other parity buffer) and this
+//       step's dynamics noise
 //   P1  all waves: L1, one 32-column tile each            (the env lanes also store the obs row)
 //   P2  all waves: L2, one 32-column tile each
 //   P3  env wave 3: the mu head; all env waves: the object update (env_object_step).  In their
@@ -933,11 +944,16 @@ template <bool kNoise, bool kDiag>
 __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p) {
     constexpr int kRows = 32;
     constexpr int kHeadWave = 3;  // an env wave: the env lanes idle while the head runs
-    __shared__ __attribute__((aligned(16))) bf16 W1s[kH * kW1s];
-    __shared__ __attribute__((aligned(16))) bf16 W3s[kOut * kW3s];
-    __shared__ __attribute__((aligned(16))) bf16 X[kRows * kXs];
-    __shared__ __attribute__((aligned(16))) bf16 H1[kRows * kHs];
-    __shared__ __attribute__((aligned(16))) bf16 H2[kRows * kHs];
+    // LDS images laid out for conflict-free 16-byte fragment reads (16-lane groups, 64 banks):
+    // the read-only W1 / W3 and the observation rows padded to a 40 / 136-dword pitch, the hidden
+    // rows unpadded with XOR-swizzled chunks (swz16; the padded 36 / 132-dword pitches of the
+    // other rollout kernels make every fragment read 2-way)
+    constexpr int kW1sW = kIn + 16, kW3sW = kH + 16, kXsW = kIn + 16, kHsW = kH;
+    __shared__ __attribute__((aligned(16))) bf16 W1s[kH * kW1sW];
+    __shared__ __attribute__((aligned(16))) bf16 W3s[kOut * kW3sW];
+    __shared__ __attribute__((aligned(16))) bf16 X[kRows * kXsW];
+    __shared__ __attribute__((aligned(16))) bf16 H1[kLsEnvs * kHsW];
+    __shared__ __attribute__((aligned(16))) bf16 H2[kLsEnvs * kHsW];
     __shared__ float MU[kLsEnvs * (kOut + 1)];
     __shared__ float LS[kActPad], SIG[kActPad], ISIG[kActPad];
     __shared__ WsDraws DR;
@@ -969,25 +985,21 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
                                                         32 * k + 8 * (lane >> 4));
     for (int c = tid; c < kH * (kIn / 8); c += kWsThreads) {
         const int row = c / (kIn / 8), col = 8 * (c % (kIn / 8));
-        *reinterpret_cast<bf16x8*>(W1s + row * kW1s + col) =
+        *reinterpret_cast<bf16x8*>(W1s + row * kW1sW + col) =
             *reinterpret_cast<const bf16x8*>(p.wbf + kBfW1a + (int64_t)row * kIn + col);
     }
     for (int c = tid; c < kOut * (kH / 8); c += kWsThreads) {
         const int row = c / (kH / 8), col = 8 * (c % (kH / 8));
-        *reinterpret_cast<bf16x8*>(W3s + row * kW3s + col) =
+        *reinterpret_cast<bf16x8*>(W3s + row * kW3sW + col) =
             *reinterpret_cast<const bf16x8*>(p.wbf + kBfW3a + (int64_t)row * kHx + col);
     }
-    for (int c = tid; c < kRows * kXs; c += kWsThreads) {
-        const int row = c / kXs, col = c % kXs;
+    for (int c = tid; c < kRows * kXsW; c += kWsThreads) {
+        const int row = c / kXsW, col = c % kXsW;
         X[c] = (row < kLsEnvs && col == kObsIn) ? (bf16)1.0f : (bf16)0.0f;
-    }
-    for (int c = tid; c < (kRows - kLsEnvs) * kHs; c += kWsThreads) {
-        H1[kLsEnvs * kHs + c] = (bf16)0.0f;
-        H2[kLsEnvs * kHs + c] = (bf16)0.0f;
     }
     const int r16 = lane & 15, g16 = lane >> 4;  // 16x16x32 fragment row / k group
     const auto w1frag = [&](int j, int k) {
-        return *reinterpret_cast<const bf16x8*>(W1s + (32 * wave + 16 * j + r16) * kW1s + 32 * k + 8 * g16);
+        return *reinterpret_cast<const bf16x8*>(W1s + (32 * wave + 16 * j + r16) * kW1sW + 32 * k + 8 * g16);
     };
     const auto w2frag = [&](int j, int k) { return w2[j][k]; };
     // step-invariant biases in registers: L2 columns 32 wave + 16 j + 4 g16 + q, head row r16
@@ -1096,8 +1108,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     // action-independent object update (env_object_step) and wave 3 the mu head: one Philox block
     // per lane, keys (KEYS) and reset counters (RW[.].rctr) of all 16 envs from LDS, values
     // written straight into the consumers' slots.
-    //   wave 4 (SIMD 0)        action noise: lane -> (env lane >> 2, block lane & 3); then the
-    //                          dynamics noise in robustness configs
+    //   wave 4 (SIMD 0)        action noise: lane -> (env lane >> 2, block lane & 3) (the
+    //                          dynamics noise is drawn in P0: obs_draws)
     //   waves 5, 6, 7 (SIMD 1, 2, 3 -- 3 also runs the head on the matrix core): group lane
     //                          g < 176 reset block g % 11 of env g / 11 (u01_53 of both halves:
     //                          joint slots 0..14 -> u1, extra slots 15..20 -> u2)
@@ -1111,19 +1123,14 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         if (wave == 4) {
             const int e = lane >> 2, blk = lane & 3;
             if ((int64_t)blockIdx.x * kLsEnvs + e >= n) return;
-#pragma unroll 1
-            for (int pass = 0; pass < (dyn_noise ? 2 : 1); ++pass) {
-                const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), pass ? kStreamDyn : kStreamPolicy,
-                                             (uint32_t)blk},
-                                       KEYS[e][2], KEYS[e][3]);
-                float nz[4];
-                box_muller(r.x, r.y, nz[0], nz[1]);
-                box_muller(r.z, r.w, nz[2], nz[3]);
-                float* dst = pass ? DR.dzn : DR.eps;
+            const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamPolicy, (uint32_t)blk},
+                                   KEYS[e][2], KEYS[e][3]);
+            float nz[4];
+            box_muller(r.x, r.y, nz[0], nz[1]);
+            box_muller(r.z, r.w, nz[2], nz[3]);
 #pragma unroll
-                for (int h = 0; h < 4; ++h)
-                    if (4 * blk + h < kAct) dst[16 * e + 4 * blk + h] = nz[h];
-            }
+            for (int h = 0; h < 4; ++h)
+                if (4 * blk + h < kAct) DR.eps[16 * e + 4 * blk + h] = nz[h];
             return;
         }
         if (wave < 5) return;
@@ -1143,7 +1150,18 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             else if (k < kReset) DR.u2[16 * e + k - kD] = u;
         }
     };
-    const auto obs_draws = [&](uint64_t ctr, int buf) {  // the observation noise of row ctr -> DR.on[buf]
+    // P0 draws of the aux lanes (counter-only, so drawn where the aux waves would wait for the env
+    // lanes' observation row): lanes s < 12 of env row eg the observation noise of row ctr (block
+    // s) into DR.on[buf]; lanes 12..15 (dyn = true) the dynamics noise of step dctr (block s - 12,
+    // normals 4 (s - 12) .. + 3) -- 64 busy lanes per aux wave, one Philox block each.
+    const auto obs_draws = [&](uint64_t ctr, int buf, bool dyn = false, uint64_t dctr = 0) {
+        if (dyn && dyn_noise && s >= 12) {
+            float nz[4];
+            normals4(dctr, kStreamDyn, s - 12, nz);
+#pragma unroll
+            for (int h = 0; h < 4; ++h)
+                if (4 * (s - 12) + h < kAct) DR.dzn[rbase + 4 * (s - 12) + h] = nz[h];
+        }
         if (obs_noise && s < (kObs + 3) / 4) {
             float nz[4];
             normals4(ctr, kStreamObs, s, nz);
@@ -1207,7 +1225,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     // without divergent branches, then at most four predicated 2-byte stores (the if / else-if
     // chain compiled to a serial walk of exec-masked regions on the env waves' critical path)
     const auto write_obs_row = [&](int buf) {  // buf: the row's noise buffer (row parity)
-        bf16* xr = X + eg * kXs;
+        bf16* xr = X + eg * kXsW;
         const auto put = [&](int j, float v, int k) {
             if (obs_noise) v = v + p.obs_noise * DR.on[buf][j][et_tid];
             xr[k] = to_bf16(v);
@@ -1221,7 +1239,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         if (s < 3) put(3, ovd, 2 * kD + 7 + s);
     };
     const auto tape_obs_row = [&](int64_t m) {
-        *reinterpret_cast<bf16x4*>(p.obs_rm + m * kIn + 4 * s) = *reinterpret_cast<const bf16x4*>(X + eg * kXs + 4 * s);
+        *reinterpret_cast<bf16x4*>(p.obs_rm + m * kIn + 4 * s) = *reinterpret_cast<const bf16x4*>(X + eg * kXsW + 4 * s);
     };
     const bool mlp = !kDiag || !(p.diag & 1), env_on = !kDiag || !(p.diag & 2);
     // ---- env lanes, P4 of step t: action, dynamics, contacts, termination, auto-reset
@@ -1367,14 +1385,14 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         if (!aux && live) write_obs_row((int)(t & 1));
         // the next observation row's noise (aux lanes, own rows; counter-only, so drawn here where
         // the aux waves wait for the env lanes' row, not in the head phase beside the draws)
-        if (aux && live && (!kDiag || !(p.diag & 256))) obs_draws(ctr + 1, (int)((t + 1) & 1));
+        if (aux && live && (!kDiag || !(p.diag & 256))) obs_draws(ctr + 1, (int)((t + 1) & 1), true, ctr);
         WS_STAMP(0);
         lds_barrier();
         if (!aux && live) tape_obs_row(m);
-        if (mlp) wave_layer16<kIn / 32, 2>(X, kXs, w1frag, 32 * wave, H1, kHs, lane);  // b: col 45
+        if (mlp) wave_layer16<kIn / 32, 2, false, true>(X, kXsW, w1frag, 32 * wave, H1, kHsW, lane);  // b: col 45
         WS_STAMP(1);
         lds_barrier();
-        if (mlp) wave_layer16<kH / 32, 2>(H1, kHs, w2frag, 32 * wave, H2, kHs, lane, b2_reg);
+        if (mlp) wave_layer16<kH / 32, 2, true, true>(H1, kHsW, w2frag, 32 * wave, H2, kHsW, lane, b2_reg);
         WS_STAMP(2);
         lds_barrier();
         if (!aux && live && env_on) env_object_step();
@@ -1386,16 +1404,16 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             bf16x8 ah[kD], bw[kD];
 #pragma unroll
             for (int k = 0; k < kD; ++k) {
-                ah[k] = *reinterpret_cast<const bf16x8*>(H2 + r16 * kHs + 32 * k + 8 * g16);
-                bw[k] = *reinterpret_cast<const bf16x8*>(W3s + r16 * kW3s + 32 * k + 8 * g16);
+                ah[k] = *reinterpret_cast<const bf16x8*>(H2 + r16 * kHsW + swz16(r16, 32 * k + 8 * g16));
+                bw[k] = *reinterpret_cast<const bf16x8*>(W3s + r16 * kW3sW + 32 * k + 8 * g16);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int k = 0; k < kH / 32; ++k) {
                 acc = mfma16(ah[k % kD], bw[k % kD], acc);
                 if (k + kD < kH / 32) {
-                    ah[k % kD] = *reinterpret_cast<const bf16x8*>(H2 + r16 * kHs + 32 * (k + kD) + 8 * g16);
-                    bw[k % kD] = *reinterpret_cast<const bf16x8*>(W3s + r16 * kW3s + 32 * (k + kD) + 8 * g16);
+                    ah[k % kD] = *reinterpret_cast<const bf16x8*>(H2 + r16 * kHsW + swz16(r16, 32 * (k + kD) + 8 * g16));
+                    bw[k % kD] = *reinterpret_cast<const bf16x8*>(W3s + r16 * kW3sW + 32 * (k + kD) + 8 * g16);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }

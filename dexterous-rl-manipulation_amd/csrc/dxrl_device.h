@@ -447,8 +447,23 @@ __device__ __forceinline__ void row_joints(float jp, float (&J)[kD]) {
         row_joints<K + 1>(jp, J);
     }
 }
+// sqrt_rn(x) < t for doubles x >= 0, t > 0, without the square root on the common path:
+// q = fl(t t); x < q (1 - 2^-40) implies sqrt(x) < t (1 - 2^-42), so the correctly rounded root
+// is < t; x > q (1 + 2^-40) implies sqrt(x) > t (1 + 2^-43), so it is >= t.  Only an x within
+// ~2^-40 relative of t^2 (a lane essentially on the contact threshold) takes the exact root.
+__device__ __forceinline__ bool sqrt_below(double x, double t) {
+    const double q = t * t;
+    if (x < q * (1.0 - 0x1p-40)) return true;
+    if (x > q * (1.0 + 0x1p-40)) return false;
+    return sqrt(x) < t;
+}
 // Lane-split contacts_of (ME:285-310) over a DPP row: lane f < 5 computes finger f from the three
 // joint positions of lanes 3f..3f+2; every lane gets the mask (ballot) and the minimum distance.
+// The contact test d_f < size * 1.5 runs on the squared distance (sqrt_below: bit-exact), and
+// dmin = min_f sqrt_rn(x_f) = sqrt_rn(min_f x_f) (the correctly rounded root is monotone), so one
+// root per row, off the mask's dependency chain; kDmin = false (the contacts of a reset state,
+// ME:176) skips it.
+template <bool kDmin = true>
 __device__ __forceinline__ uint32_t row_contacts(float jp, const double op[3], double size, int s, int gbit,
                                                  double& dmin, float g3[3]) {
     // finger s's joints (lanes 3s .. 3s + 2 of the row; lanes s >= kF take finger 0's) through the
@@ -462,15 +477,20 @@ __device__ __forceinline__ uint32_t row_contacts(float jp, const double op[3], d
     for (int j = 1; j < kJ; ++j) sum = sum + g3[j];
     const double tip = (double)(sum * kC01);
     const double dx = tip - op[0], dy = tip - op[1], dz = tip - op[2];
-    const double d = sqrt((dx * dx + dy * dy) + dz * dz);
-    const bool hit = s < kF && d < size * 1.5;
+    const double x = (dx * dx + dy * dy) + dz * dz;
+    const bool hit = s < kF && sqrt_below(x, size * 1.5);
     const uint32_t mask = (uint32_t)(__ballot(hit) >> gbit) & ((1u << kF) - 1u);
-    dmin = row_bcast<0>(d);
-    const double d1 = row_bcast<1>(d), d2 = row_bcast<2>(d), d3 = row_bcast<3>(d), d4 = row_bcast<4>(d);
-    dmin = d1 < dmin ? d1 : dmin;
-    dmin = d2 < dmin ? d2 : dmin;
-    dmin = d3 < dmin ? d3 : dmin;
-    dmin = d4 < dmin ? d4 : dmin;
+    if constexpr (kDmin) {
+        double xm = row_bcast<0>(x);
+        const double x1 = row_bcast<1>(x), x2 = row_bcast<2>(x), x3 = row_bcast<3>(x), x4 = row_bcast<4>(x);
+        xm = x1 < xm ? x1 : xm;
+        xm = x2 < xm ? x2 : xm;
+        xm = x3 < xm ? x3 : xm;
+        xm = x4 < xm ? x4 : xm;
+        dmin = sqrt(xm);
+    } else {
+        dmin = 0.0;
+    }
     return mask;
 }
 __device__ __forceinline__ void row_object(double opd, double op[3]) {

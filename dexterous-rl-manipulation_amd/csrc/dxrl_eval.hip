@@ -415,7 +415,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_ls(const dxrl_curriculum*
         double op3[3], dmin;
         float g3[3];
         row_object(opd, op3);
-        flags |= row_contacts(jp, op3, size, s, gbit, dmin, g3);  // ME:176
+        flags |= row_contacts<false>(jp, op3, size, s, gbit, dmin, g3);  // ME:176 (no dmin)
         otraj = a.obs_traj ? a.obs_traj + rec * (int64_t)(a.max_steps + 1) * kObs : nullptr;
         atraj = a.act_traj ? a.act_traj + rec * (int64_t)a.max_steps * kD : nullptr;
         if (otraj) write_obs_row(otraj);

@@ -1155,34 +1155,38 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     // s) into DR.on[buf]; lanes 12..15 (dyn = true) the dynamics noise of step dctr (block s - 12,
     // normals 4 (s - 12) .. + 3) -- 64 busy lanes per aux wave, one Philox block each.
     const auto obs_draws = [&](uint64_t ctr, int buf, bool dyn = false, uint64_t dctr = 0) {
-        if (dyn && dyn_noise && s >= 12) {
-            float nz[4];
-            normals4(dctr, kStreamDyn, s - 12, nz);
+        constexpr int kOb = (kObs + 3) / 4;  // 12 observation blocks per row
+        const bool is_obs = s < kOb, want = is_obs ? obs_noise : (dyn && dyn_noise);
+        if (!(obs_noise || (dyn && dyn_noise))) return;
+        // one Philox block per lane, the stream / counter / block selected per lane, so the wave
+        // runs ONE Philox + Box-Muller sequence (lanes 12..15 branching into a second stream
+        // would serialise the two)
+        float nz[4];
+        normals4(is_obs ? ctr : dctr, is_obs ? kStreamObs : kStreamDyn, is_obs ? s : s - kOb, nz);
+        if (!want) return;
+        if (!is_obs) {
 #pragma unroll
             for (int h = 0; h < 4; ++h)
-                if (4 * (s - 12) + h < kAct) DR.dzn[rbase + 4 * (s - 12) + h] = nz[h];
+                if (4 * (s - kOb) + h < kAct) DR.dzn[rbase + 4 * (s - kOb) + h] = nz[h];
+            return;
         }
-        if (obs_noise && s < (kObs + 3) / 4) {
-            float nz[4];
-            normals4(ctr, kStreamObs, s, nz);
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const int k = 4 * s + h;
-                if (k < kObs) {
-                    int ln, j;
-                    obs_slot(k, ln, j);
-                    DR.on[buf][j][rbase + ln] = nz[h];
-                }
+        for (int h = 0; h < 4; ++h) {
+            const int k = 4 * s + h;
+            if (k < kObs) {
+                int ln, j;
+                obs_slot(k, ln, j);
+                DR.on[buf][j][rbase + ln] = nz[h];
             }
-            if (kDiag && p.obs_noise_tape) {  // parity tape: the value write_obs_row adds (row ctr - iteration T)
-                const int64_t row = (int64_t)(ctr - p.iteration * (uint64_t)T);
-                float4 v;
-                v.x = 4 * s + 0 < kObs ? p.obs_noise * nz[0] : 0.0f;
-                v.y = 4 * s + 1 < kObs ? p.obs_noise * nz[1] : 0.0f;
-                v.z = 4 * s + 2 < kObs ? p.obs_noise * nz[2] : 0.0f;
-                v.w = 4 * s + 3 < kObs ? p.obs_noise * nz[3] : 0.0f;
-                *reinterpret_cast<float4*>(p.obs_noise_tape + (row * n + i) * kObsNoiseLd + 4 * s) = v;
-            }
+        }
+        if (kDiag && p.obs_noise_tape) {  // parity tape: the value write_obs_row adds (row ctr - iteration T)
+            const int64_t row = (int64_t)(ctr - p.iteration * (uint64_t)T);
+            float4 v;
+            v.x = 4 * s + 0 < kObs ? p.obs_noise * nz[0] : 0.0f;
+            v.y = 4 * s + 1 < kObs ? p.obs_noise * nz[1] : 0.0f;
+            v.z = 4 * s + 2 < kObs ? p.obs_noise * nz[2] : 0.0f;
+            v.w = 4 * s + 3 < kObs ? p.obs_noise * nz[3] : 0.0f;
+            *reinterpret_cast<float4*>(p.obs_noise_tape + (row * n + i) * kObsNoiseLd + 4 * s) = v;
         }
     };
     // ---- aux: the dense reward (RS:50-187) and the episode bookkeeping of a finished step
@@ -1337,7 +1341,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             row_object(opd, op3);
             double dmin;
             float g3[3];
-            flags |= row_contacts(jp, op3, size, s, gbit, dmin, g3);
+            flags |= row_contacts<false>(jp, op3, size, s, gbit, dmin, g3);  // ME:176 (no dmin)
             ++rctr;
         }
         if (s == 0) RW[t & 1][eg].rctr = rctr;

@@ -317,3 +317,26 @@ def test_reward_plugin_compute_has_no_cpu_fallback():
         R.RewardShaping().compute(np.zeros(15, np.float32), np.zeros((5, 3)), np.zeros(3), np.zeros(5, np.float32), 5, 3)
     with pytest.raises(N.NativeError):
         R.SparseReward().compute(None, None, None, np.zeros(5, np.float32), 5, 3)
+
+
+def test_sqrt_below_margin_test_is_exact():
+    """csrc/dxrl_device.h sqrt_below: the contact test sqrt_rn(x) < t decided on x against
+    q (1 -+ 2^-40) with q = fl(t t), the exact root only inside that window.  Restated in f64
+    NumPy (IEEE, correctly rounded sqrt) on values straddling the threshold: the margin
+    branches never disagree with the root.  Also min_f sqrt_rn(x_f) == sqrt_rn(min_f x_f)."""
+    rng = np.random.default_rng(3)
+    t = rng.uniform(0.003, 0.5, 200_000) * 1.5
+    q = t * t
+    rel = rng.choice([1e-18, 1e-16, 1e-14, 1e-12, 1e-9, 1e-6, 1e-3, 0.3], t.size) * rng.choice([-1, 1], t.size)
+    x = np.concatenate([q * (1 + rel), q, np.nextafter(q, 0), np.nextafter(q, 1), (np.nextafter(t, 0)) ** 2,
+                        (np.nextafter(t, 1)) ** 2])
+    tt = np.concatenate([t] * 6)
+    qq = tt * tt
+    truth = np.sqrt(x) < tt
+    lo, hi = x < qq * (1.0 - 2.0 ** -40), x > qq * (1.0 + 2.0 ** -40)
+    assert not (lo & hi).any()
+    assert truth[lo].all() and not truth[hi].any()
+    fast = np.where(lo, True, np.where(hi, False, truth))
+    assert np.array_equal(fast, truth)
+    xs = rng.uniform(0, 0.1, (100_000, 5))
+    assert np.array_equal(np.sqrt(xs).min(1), np.sqrt(xs.min(1)))

@@ -51,6 +51,36 @@ int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, 
                     int splits, float* partial, float* out, hipStream_t st, int64_t ldo, int reduce = 1,
                     int* nslabs = nullptr);
 
+// s += partial[k * stride4 + i] for k = k0 .. k1 - 1, in that order, with the loads issued in
+// batches of 8 ahead of their adds (the plain loop waits out one load latency per slab: the
+// reductions read their slabs from the Infinity Cache at a fraction of its bandwidth).  Same adds
+// in the same order, so bit for bit the plain loop's sum.
+__device__ __forceinline__ float4 ordered_slab_sum(const float4* __restrict__ partial, int64_t stride4, int64_t i,
+                                                   int k0, int k1, float4 s) {
+    constexpr int kB = 8;
+    int k = k0;
+    for (; k + kB <= k1; k += kB) {
+        float4 v[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) v[u] = partial[(int64_t)(k + u) * stride4 + i];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            s.x += v[u].x;
+            s.y += v[u].y;
+            s.z += v[u].z;
+            s.w += v[u].w;
+        }
+    }
+    for (; k < k1; ++k) {
+        const float4 v = partial[(int64_t)k * stride4 + i];
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+    }
+    return s;
+}
+
 // One 256-thread block of the two-level fixed-order slab sum (k_slab_reduce2_4): float4 columns
 // 16 blk .. 16 blk + 15 of z slabs; 16 groups of threads sum contiguous slab ranges, then group 0
 // adds the 16 group sums in group order.  grp: the block's [16][16] float4 scratch in LDS.
@@ -62,15 +92,7 @@ __device__ __forceinline__ void slab_reduce_block(const float4* __restrict__ par
     const int64_t i = blk * kRX + x;
     const int k0 = (int)((int64_t)g * z / kReduceGroups), k1 = (int)((int64_t)(g + 1) * z / kReduceGroups);
     float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (i < slab4) {
-        for (int k = k0; k < k1; ++k) {
-            const float4 v = partial[(int64_t)k * slab4 + i];
-            s.x += v.x;
-            s.y += v.y;
-            s.z += v.z;
-            s.w += v.w;
-        }
-    }
+    if (i < slab4) s = ordered_slab_sum(partial, slab4, i, k0, k1, s);
     grp[g][x] = s;
     __syncthreads();
     if (g != 0 || i >= slab4) return;

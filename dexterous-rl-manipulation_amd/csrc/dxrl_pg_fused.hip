@@ -1114,8 +1114,7 @@ __device__ __forceinline__ void fused_reduce_block(const float4* __restrict__ pa
     if (z > kReduceGroups) {
         const int k0 = (int)((int64_t)g * z / kReduceGroups), k1 = (int)((int64_t)(g + 1) * z / kReduceGroups);
         float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (i < kSlab4)
-            for (int k = k0; k < k1; ++k) s = add(s, partial[(int64_t)k * kSlab4 + i]);
+        if (i < kSlab4) s = ordered_slab_sum(partial, kSlab4, i, k0, k1, s);  // == the in-order loop
         grp[g][x] = s;
         __syncthreads();
         if (g != 0 || i >= kSlab4) return;
@@ -1123,7 +1122,7 @@ __device__ __forceinline__ void fused_reduce_block(const float4* __restrict__ pa
         for (int q = 0; q < kReduceGroups; ++q) r = add(r, grp[q][x]);
     } else {
         if (g != 0 || i >= kSlab4) return;
-        for (int k = 0; k < z; ++k) r = add(r, partial[(int64_t)k * kSlab4 + i]);
+        r = ordered_slab_sum(partial, kSlab4, i, 0, z, r);
     }
     const int j = (int)(4 * i);
     fused_scatter_one(j, r.x, gW1, gW3, gLs, gW2, ent_coef);

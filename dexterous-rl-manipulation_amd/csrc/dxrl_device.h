@@ -420,7 +420,10 @@ __device__ __forceinline__ double reset_uniform_at(int k, uint32_t k0, uint32_t 
 // call only where the whole row is active.
 template <int K>
 __device__ __forceinline__ uint32_t row_bcast_u32(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x150 + K, 0xF, 0xF, false);  // row_newbcast:K
+    // every lane of the row reads a valid source lane, so the "old" operand is never used: the
+    // undefined-old form (mov_dpp) spares the v_mov_b32 0 the update_dpp(0, ...) form put in front
+    // of each broadcast
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + K, 0xF, 0xF, true);  // row_newbcast:K
 }
 template <int K>
 __device__ __forceinline__ float row_bcast(float x) {

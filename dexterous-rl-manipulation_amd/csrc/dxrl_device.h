@@ -131,6 +131,15 @@ __device__ __forceinline__ float count_over_f_f32(uint32_t k) {
     return r;
 }
 
+// x / 5 in f32, correctly rounded, without the division sequence (-fhip-fp32-correctly-rounded-
+// divide-sqrt compiles x / 5.0f to ~10 dependent instructions): RN32(RN64(x * RN64(0.2))).  For a
+// normal f32 x = M 2^k the exact quotient is at least ulp(q) / 10 from every f32 midpoint (the
+// numerator of q - mid is a nonzero multiple of 2^(j - 1) over 5), while the f64 product is within
+// ~2^-52 q of x / 5, so both roundings land on the same f32 (tests/test_host_logic.py checks it
+// against IEEE f32 division over whole binades).
+static_assert(kF == 5, "div_f: the finger count's reciprocal constant");
+__device__ __forceinline__ float div_f(float x) { return (float)((double)x * 0.2); }
+
 // RS:101-187 dense terms + weighted total (RS:84-89); updates prev contacts.
 __device__ __forceinline__ double dense_reward(Env& e, uint32_t c, double dmin, const Weights& w, double comp[4]) {
     const double dist = exp(-5.0 * dmin);                 // RS:111-116
@@ -147,8 +156,8 @@ __device__ __forceinline__ double dense_reward(Env& e, uint32_t c, double dmin, 
         }
         sum = sum + (-acc);
     }
-    const float avg = sum / (float)kF;
-    const float clo = clipf(avg / (float)kF, 0.0f, 1.0f);
+    const float avg = div_f(sum);                         // np.mean(...)  (f32 / 5)
+    const float clo = clipf(div_f(avg), 0.0f, 1.0f);      // avg / num_fingers
     float st = 0.0f;                                      // RS:166-187
     if (e.flags & kHasPrev) {
         const uint32_t prev = (e.flags >> kPrevShift) & 0xFFu;

@@ -232,7 +232,7 @@ __global__ void k_reward_compute(int64_t count, bool dense, Weights w, const flo
         float ch = 0.0f;
 #pragma unroll
         for (int f = 0; f < kF; ++f) ch = ch + fabsf(c[f] - prev[i * kF + f]);
-        st = clipf(1.0f - ch / (float)kF, 0.0f, 1.0f);
+        st = clipf(1.0f - div_f(ch), 0.0f, 1.0f);
     }
 #pragma unroll
     for (int f = 0; f < kF; ++f) prev[i * kF + f] = c[f];

@@ -554,8 +554,8 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_ls(const dxrl_curriculum*
                 if (g3[j] < 0.0f) nacc = nacc + g3[j];
             float sum = 0.0f;
             row_neg_sum_in_order<kF>(nacc, sum);
-            const float avg = sum / (float)kF;
-            const float clo = clipf(avg / (float)kF, 0.0f, 1.0f);
+            const float avg = div_f(sum);
+            const float clo = clipf(div_f(avg), 0.0f, 1.0f);
             float st = 0.0f;
             if (flags & kHasPrev) {
                 const uint32_t prev = (flags >> kPrevShift) & 0xFFu;

@@ -769,8 +769,8 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
             float sum = 0.0f;
 #pragma unroll
             for (int f = 0; f < kF; ++f) sum = sum + (-gx[kGxNacc + f]);
-            const float avg = sum / (float)kF;
-            const float clo = clipf(avg / (float)kF, 0.0f, 1.0f);
+            const float avg = div_f(sum);
+            const float clo = clipf(div_f(avg), 0.0f, 1.0f);
             float st = 0.0f;
             if (flags & kHasPrev) {
                 const uint32_t prev = (flags >> kPrevShift) & 0xFFu;
@@ -1197,8 +1197,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         float sum = 0.0f;
 #pragma unroll
         for (int f = 0; f < kF; ++f) sum = sum + (-w.nacc[f]);
-        const float avg = sum / (float)kF;
-        const float clo = clipf(avg / (float)kF, 0.0f, 1.0f);
+        const float avg = div_f(sum);
+        const float clo = clipf(div_f(avg), 0.0f, 1.0f);
         float st = 0.0f;
         if (w.prev != 0x100u) {
             float ch = 0.0f;

@@ -340,3 +340,18 @@ def test_sqrt_below_margin_test_is_exact():
     assert np.array_equal(fast, truth)
     xs = rng.uniform(0, 0.1, (100_000, 5))
     assert np.array_equal(np.sqrt(xs).min(1), np.sqrt(xs.min(1)))
+
+
+def test_div_by_five_without_division_is_correctly_rounded():
+    """csrc/dxrl_device.h div_f: f32(f64(x) * 0.2) == x / 5 in IEEE f32 (correctly rounded, as
+    NumPy's f32 division and -fhip-fp32-correctly-rounded-divide-sqrt give) -- every f32 of the
+    binades [2^-8, 2^5) (the closure / stability arguments lie in [0, 15]) plus a log-uniform
+    sample over the normal range."""
+    f32 = np.float32
+    m = np.arange(1 << 23, dtype=np.uint32)
+    for e in range(-8, 5):
+        x = ((m | np.uint32(127 + e) << np.uint32(23)).view(np.float32))
+        assert np.array_equal((x.astype(np.float64) * 0.2).astype(f32), x / f32(5)), e
+    rng = np.random.default_rng(1)
+    x = (2.0 ** rng.uniform(-126, 127, 4_000_000)).astype(f32)
+    assert np.array_equal((x.astype(np.float64) * 0.2).astype(f32), x / f32(5))

@@ -469,8 +469,19 @@ __device__ __forceinline__ bool sqrt_below(double x, double t) {
     if (x > q * (1.0 + 0x1p-40)) return false;
     return sqrt(x) < t;
 }
-// Lane-split contacts_of (ME:285-310) over a DPP row: lane f < 5 computes finger f from the three
-// joint positions of lanes 3f..3f+2; every lane gets the mask (ballot) and the minimum distance.
+// lane s receives lane s + N's value within its 16-lane row (row_shl:N; lanes past the row end
+// read 0 -- they are never finger lanes)
+template <int N>
+__device__ __forceinline__ float row_shl(float x) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x100 + N, 0xF, 0xF, true));
+}
+// finger lanes of a row: lane 3 f holds finger f's joints 3 f .. 3 f + 2 after two row shifts
+__device__ __forceinline__ bool finger_lane(int s) { return s < kD && s % kJ == 0; }
+// Lane-split contacts_of (ME:285-310) over a DPP row: finger lane 3f gathers its finger's three
+// joint positions with two row shifts (no LDS round trip: the ds_bpermute gather sat on the step's
+// dependent chain twice per reset step) and sums them in the reference's order; every lane gets
+// the mask (ballot, the finger lanes' bits compressed to bit f) and the minimum distance.
+// g3: the finger's joints (finger lanes).
 // The contact test d_f < size * 1.5 runs on the squared distance (sqrt_below: bit-exact), and
 // dmin = min_f sqrt_rn(x_f) = sqrt_rn(min_f x_f) (the correctly rounded root is monotone), so one
 // root per row, off the mask's dependency chain; kDmin = false (the contacts of a reset state,
@@ -478,23 +489,20 @@ __device__ __forceinline__ bool sqrt_below(double x, double t) {
 template <bool kDmin = true>
 __device__ __forceinline__ uint32_t row_contacts(float jp, const double op[3], double size, int s, int gbit,
                                                  double& dmin, float g3[3]) {
-    // finger s's joints (lanes 3s .. 3s + 2 of the row; lanes s >= kF take finger 0's) through the
-    // LDS crossbar: three ds_bpermute instead of 15 row broadcasts and 12 selects on the VALU
-    const int src = gbit + (s < kF ? kJ * s : 0);
-#pragma unroll
-    for (int j = 0; j < kJ; ++j)
-        g3[j] = __int_as_float(__builtin_amdgcn_ds_bpermute((src + j) << 2, __float_as_int(jp)));
-    float sum = g3[0];
-#pragma unroll
-    for (int j = 1; j < kJ; ++j) sum = sum + g3[j];
+    static_assert(kJ == 3 && kF * kJ <= 16, "finger lanes 3 f of a 16-lane row");
+    g3[0] = jp;
+    g3[1] = row_shl<1>(jp);
+    g3[2] = row_shl<2>(jp);
+    const float sum = (g3[0] + g3[1]) + g3[2];  // np.sum of the finger's f32 joints, in order
     const double tip = (double)(sum * kC01);
     const double dx = tip - op[0], dy = tip - op[1], dz = tip - op[2];
     const double x = (dx * dx + dy * dy) + dz * dz;
-    const bool hit = s < kF && sqrt_below(x, size * 1.5);
-    const uint32_t mask = (uint32_t)(__ballot(hit) >> gbit) & ((1u << kF) - 1u);
+    const bool hit = finger_lane(s) && sqrt_below(x, size * 1.5);
+    const uint32_t r16 = (uint32_t)(__ballot(hit) >> gbit);  // bit 3 f: finger f
+    const uint32_t mask = (r16 & 1u) | ((r16 >> 2) & 2u) | ((r16 >> 4) & 4u) | ((r16 >> 6) & 8u) | ((r16 >> 8) & 16u);
     if constexpr (kDmin) {
         double xm = row_bcast<0>(x);
-        const double x1 = row_bcast<1>(x), x2 = row_bcast<2>(x), x3 = row_bcast<3>(x), x4 = row_bcast<4>(x);
+        const double x1 = row_bcast<3>(x), x2 = row_bcast<6>(x), x3 = row_bcast<9>(x), x4 = row_bcast<12>(x);
         xm = x1 < xm ? x1 : xm;
         xm = x2 < xm ? x2 : xm;
         xm = x3 < xm ? x3 : xm;
@@ -511,12 +519,13 @@ __device__ __forceinline__ void row_object(double opd, double op[3]) {
     op[2] = row_bcast<2>(opd);
 }
 
-// acc = ((acc + (-x_0)) + (-x_1)) + ...  (the closure term's sum of finger sums, RS:147-162)
-template <int N, int K = 0>
-__device__ __forceinline__ void row_neg_sum_in_order(float x, float& acc) {
-    if constexpr (K < N) {
-        acc = acc + (-row_bcast<K>(x));
-        row_neg_sum_in_order<N, K + 1>(x, acc);
+// acc = ((acc + (-x_0)) + (-x_1)) + ...  over the finger lanes 0, 3, .., 12 (x_f on lane 3 f: the
+// closure term's sum of finger sums, RS:147-162)
+template <int K = 0>
+__device__ __forceinline__ void row_neg_sum_fingers(float x, float& acc) {
+    if constexpr (K < kF) {
+        acc = acc + (-row_bcast<kJ * K>(x));
+        row_neg_sum_fingers<K + 1>(x, acc);
     }
 }
 

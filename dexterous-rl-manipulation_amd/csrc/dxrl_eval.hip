@@ -553,7 +553,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_ls(const dxrl_curriculum*
             for (int j = 0; j < kJ; ++j)
                 if (g3[j] < 0.0f) nacc = nacc + g3[j];
             float sum = 0.0f;
-            row_neg_sum_in_order<kF>(nacc, sum);
+            row_neg_sum_fingers(nacc, sum);  // nacc of finger f on lane 3 f
             const float avg = div_f(sum);
             const float clo = clipf(div_f(avg), 0.0f, 1.0f);
             float st = 0.0f;

@@ -1294,7 +1294,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
 #pragma unroll
             for (int j = 0; j < kJ; ++j)
                 if (g3[j] < 0.0f) nacc = nacc + g3[j];
-            if (s < kF) rw.nacc[s] = nacc;
+            if (finger_lane(s)) rw.nacc[s / kJ] = nacc;  // finger f on lane 3 f
             if (s == 0) {
                 rw.dmin = dmin;
                 rw.c = c;

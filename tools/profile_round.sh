@@ -29,7 +29,7 @@ if [ -z "${SKIP_PMC:-}" ]; then
   python tools/pmc_report.py "$O/pmc_fetch/**/*counter_collection.csv" "$O/pmc_write/**/*counter_collection.csv" 4194304 $O/pmc_step_kernel.json > /dev/null
   # this round's PMC file where bench.py reads roofline.traffic from (profiles/rNN/), so the bench
   # lines below cite traffic measured at the same HEAD
-  mkdir -p profiles/${ROUND:-r03} && cp $O/pmc_step_kernel.json profiles/${ROUND:-r03}/pmc_step_kernel.json
+  mkdir -p profiles/${ROUND:-r04} && cp $O/pmc_step_kernel.json profiles/${ROUND:-r04}/pmc_step_kernel.json
   step pmc_mfma 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/pmc_mfma -o run -- python3 tools/prof_pg_iter.py
   python tools/pmc_kernels.py "$O/pmc_mfma/**/*counter_collection.csv" > $O/pmc_mfma.json
   # VALU / LDS / wait view of the same iterations (8 SQ counters: one pass)

@@ -22,9 +22,17 @@ src_root = os.path.join(ROOT, "ab", f"_src_{name}")  # per variant: builds may r
 if os.path.exists(src_root):
     shutil.rmtree(src_root)
 csrc = os.path.join(src_root, "pkg", "csrc")
-shutil.copytree(B.CSRC, csrc)
-os.makedirs(os.path.join(src_root, "include"))
-shutil.copy(os.path.join(ROOT, "include", "dxrl.h"), os.path.join(src_root, "include", "dxrl.h"))
+rev = os.environ.get("SRC_REV")  # build the kernels of an older commit (same C ABI required)
+if rev:
+    os.makedirs(src_root)
+    for sub, dst in (("dexterous-rl-manipulation_amd/csrc", csrc), ("include", os.path.join(src_root, "include"))):
+        os.makedirs(dst)
+        tar = subprocess.run(["git", "archive", rev, sub], cwd=ROOT, check=True, capture_output=True).stdout
+        subprocess.run(["tar", "-x", "--strip-components", str(sub.count("/") + 1), "-C", dst], input=tar, check=True)
+else:
+    shutil.copytree(B.CSRC, csrc)
+    os.makedirs(os.path.join(src_root, "include"))
+    shutil.copy(os.path.join(ROOT, "include", "dxrl.h"), os.path.join(src_root, "include", "dxrl.h"))
 for k in range(0, len(subs), 3):
     fn, old, new = subs[k], open(subs[k + 1]).read(), open(subs[k + 2]).read()
     path = os.path.join(csrc, fn)

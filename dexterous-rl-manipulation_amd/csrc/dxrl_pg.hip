@@ -908,13 +908,15 @@ __device__ __forceinline__ void lds_barrier() {
 // the head phase, read before the next head phase); the observation noise is double-buffered by
 // row parity (row t + 1's is written in step t's P0 while the env lanes read row t's).  The reward inputs (WsReward) are double-buffered
 // by step parity: the env lanes write step t's while the aux lanes settle step t-1's.
-struct WsDraws {
+struct __attribute__((aligned(16))) WsDraws {
     float eps[256], dzn[256], on[2][4][256];  // on: double-buffered by observation row parity
     double u1[256], u2[256];
 };
-struct WsSampler {     // one env lane's extra reset draw: has ? lo + span u : cst
-    double lo, span, cst;
-    int32_t has, pad;
+// one env lane's extra reset draw (config.py:44-113 samplers): lo + span u with a range, the
+// constant (lo = cst, span = NaN: u is never NaN) without one -- structure of arrays, so the reset
+// path's two reads are conflict-free 8-byte loads
+struct WsSamplers {
+    double lo[256], span[256];
 };
 struct WsReward {      // an env's dense-reward inputs and episode end of one step
     double dmin;
@@ -958,7 +960,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     __shared__ float LS[kActPad], SIG[kActPad], ISIG[kActPad];
     __shared__ WsDraws DR;
     __shared__ WsReward RW[2][kLsEnvs];
-    __shared__ WsSampler RSMP[kWsThreads / 2];
+    __shared__ WsSamplers RSMP;
     __shared__ uint32_t KEYS[kLsEnvs][4];           // per env: reset key ek0, ek1, policy key pk0, pk1
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool aux = wave >= 4;
@@ -1046,7 +1048,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     }
     const int s2 = s < DXRL_RESET_EXTRA ? s : 0;
     // this lane's extra reset sampler (config.py:44-113) -- read only when an episode ends, so
-    // kept in LDS rather than in registers: RSMP[et_tid] = {lo, hi - lo, constant, has range}
+    // kept in LDS rather than in registers: RSMP.lo / span[et_tid] = {lo, hi - lo} or {constant, NaN}
     double lo2 = 0.0, hi2 = 0.0, cst2 = 0.0;
     bool has2 = true, fric64 = false;
     if (live && !aux) {
@@ -1059,7 +1061,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         hi2 = rg[1];
         cst2 = s2 == 0 ? cu.object_size : s2 == 1 ? cu.object_mass : cu.friction_coefficient;
         has2 = s2 == 0 ? cu.has_size_range != 0 : s2 == 1 ? cu.has_mass_range != 0 : s2 == 2 ? cu.has_friction_range != 0 : true;
-        RSMP[et_tid] = WsSampler{lo2, hi2 - lo2, cst2, has2 ? 1 : 0};
+        RSMP.lo[et_tid] = has2 ? lo2 : cst2;
+        RSMP.span[et_tid] = has2 ? hi2 - lo2 : __builtin_nan("");
         fric64 = cu.friction_is_f64_scalar != 0;
     }
     const int sa = s < kAct ? s : 0;
@@ -1125,12 +1128,12 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             if ((int64_t)blockIdx.x * kLsEnvs + e >= n) return;
             const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamPolicy, (uint32_t)blk},
                                    KEYS[e][2], KEYS[e][3]);
-            float nz[4];
-            box_muller(r.x, r.y, nz[0], nz[1]);
-            box_muller(r.z, r.w, nz[2], nz[3]);
-#pragma unroll
-            for (int h = 0; h < 4; ++h)
-                if (4 * blk + h < kAct) DR.eps[16 * e + 4 * blk + h] = nz[h];
+            float4 nz;
+            box_muller(r.x, r.y, nz.x, nz.y);
+            box_muller(r.z, r.w, nz.z, nz.w);
+            // one 16-byte store per lane (slot 15 of the row is never read: kAct = 15); four
+            // 4-byte stores at a 16-byte lane stride were 4-way bank conflicts
+            *reinterpret_cast<float4*>(&DR.eps[16 * e + 4 * blk]) = nz;
             return;
         }
         if (wave < 5) return;
@@ -1164,10 +1167,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         float nz[4];
         normals4(is_obs ? ctr : dctr, is_obs ? kStreamObs : kStreamDyn, is_obs ? s : s - kOb, nz);
         if (!want) return;
-        if (!is_obs) {
-#pragma unroll
-            for (int h = 0; h < 4; ++h)
-                if (4 * (s - kOb) + h < kAct) DR.dzn[rbase + 4 * (s - kOb) + h] = nz[h];
+        if (!is_obs) {  // one 16-byte store (slot 15 never read), as the action noise
+            *reinterpret_cast<float4*>(&DR.dzn[rbase + 4 * (s - kOb)]) = float4{nz[0], nz[1], nz[2], nz[3]};
             return;
         }
 #pragma unroll
@@ -1319,8 +1320,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         if (d) {
             // ---- env_reset_philox, lane-split: lane s holds slot s (joint) and slot 15 + s
             const double u1 = DR.u1[et_tid], u2 = DR.u2[et_tid];
-            const WsSampler sm = RSMP[et_tid];
-            const double v2 = sm.has ? sm.lo + sm.span * u2 : sm.cst;  // config.py:44-113 samplers
+            const double slo = RSMP.lo[et_tid], span = RSMP.span[et_tid];
+            const double v2 = span == span ? slo + span * u2 : slo;  // config.py:44-113 samplers
             if (s < kD) {
                 jp = (float)(-0.1 + (0.1 - -0.1) * u1);
                 jv = 0.0f;

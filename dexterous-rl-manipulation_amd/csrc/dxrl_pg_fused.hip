@@ -172,20 +172,15 @@ __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int kst, i
 // MFMA chain runs the epilogue of tile mt - 1 issues into its gaps one value pair at a time
 // (epi(acc, mt, p): pair p = 0..7 of the lane's 16 values, group p >> 1).  Two accumulators live
 // instead of MT.  Per output the k order -- and so every bit -- is the same as fwd_run's.
-template <int KS, int kLda, int MT, typename Epi, typename Hook = NoHook, typename KHook = NoKHook>
-__device__ __forceinline__ void fwd_pipe(WPre<KS>& w, const bf16* A, int lane, Epi& epi, Hook hook = Hook{},
-                                         bool no_mfma = false, KHook khook = KHook{}) {
+// (fwd_pipe_w: the same with all KS weight fragments already in registers -- the forward-only
+// pass keeps them resident for the launch)
+template <int KS, int kLda, int MT, typename Epi, typename KHook = NoKHook>
+__device__ __forceinline__ void fwd_pipe_w(const bf16x8 (&wf)[KS], const bf16* A, int lane, Epi& epi,
+                                           bool no_mfma = false, KHook khook = KHook{}) {
     static_assert(KS >= 4 && KS % 4 == 0, "pair schedule assumes KS in {4, 8, 16, ...}");
     const int r = lane & 31, h = lane >> 5;
-    constexpr int kD = WPre<KS>::kD;
     constexpr int kPairsPerK = KS >= 8 ? 1 : 8 / KS;  // epilogue pairs issued per k-step
     constexpr int kKPerPair = KS >= 8 ? KS / 8 : 1;   // k-steps per epilogue pair
-    bf16x8 wf[KS];
-#pragma unroll
-    for (int k = 0; k < kD; ++k) wf[k] = w.wf[k];
-#pragma unroll
-    for (int k = kD; k < KS; ++k) wf[k] = w.wp[64 * k];
-    hook();  // loads the caller wants behind the last weight fragment (vmcnt retires in order)
     const bf16* ap = A + r * kLda + 8 * h;
     f32x16 acc, prev;
     // activation fragments kBD k-steps ahead (one MFMA per k-step now covers a read, not four)
@@ -219,6 +214,18 @@ __device__ __forceinline__ void fwd_pipe(WPre<KS>& w, const bf16* A, int lane, E
     epi.prime(MT - 1);
 #pragma unroll
     for (int q = 0; q < 8; ++q) epi(prev, MT - 1, q);
+}
+template <int KS, int kLda, int MT, typename Epi, typename Hook = NoHook, typename KHook = NoKHook>
+__device__ __forceinline__ void fwd_pipe(WPre<KS>& w, const bf16* A, int lane, Epi& epi, Hook hook = Hook{},
+                                         bool no_mfma = false, KHook khook = KHook{}) {
+    constexpr int kD = WPre<KS>::kD;
+    bf16x8 wf[KS];
+#pragma unroll
+    for (int k = 0; k < kD; ++k) wf[k] = w.wf[k];
+#pragma unroll
+    for (int k = kD; k < KS; ++k) wf[k] = w.wp[64 * k];
+    hook();  // loads the caller wants behind the last weight fragment (vmcnt retires in order)
+    fwd_pipe_w<KS, kLda, MT>(wf, A, lane, epi, no_mfma, khook);
 }
 
 // fwd_pipe epilogues.  EpiTanh: tanh(acc + bias) -> bf16 H rows (store_hidden, pair by pair);
@@ -360,6 +367,9 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #ifndef DXRL_HEAD_PF
 #define DXRL_HEAD_PF 1
 #endif
+#ifndef DXRL_FWD_RESIDENT_W
+#define DXRL_FWD_RESIDENT_W 1
+#endif
 #ifndef DXRL_FUSED_PRIO
 #define DXRL_FUSED_PRIO 1
 #endif
@@ -457,6 +467,35 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             st_last = t_;                                                                        \
         }                                                                                        \
     } while (0)
+    // forward-only pass (critic values): this wave's W1 / W2 fragments stay in registers for the
+    // whole launch (80 VGPRs; the train instantiations have no room for them) instead of streaming
+    // 160 KB of weight fragments from L2 per tile and workgroup
+    constexpr bool kResW = !kTrain && kNT == 1 && DXRL_FWD_RESIDENT_W && DXRL_L2_PIPE;
+    bf16x8 w1res[kResW ? kIn / 16 : 1], w2res[kResW ? kH / 16 : 1];
+    if constexpr (kResW) {
+        const gbf16x8* p1 = (const gbf16x8*)p.W1 + (int64_t)ft0 * (kIn / 16) * 64 + lane;
+        const gbf16x8* p2 = (const gbf16x8*)p.W2 + (int64_t)ft0 * (kH / 16) * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < kIn / 16; ++k) w1res[k] = p1[64 * k];
+#pragma unroll
+        for (int k = 0; k < kH / 16; ++k) w2res[k] = p2[64 * k];
+    }
+    // ... and so do the layer-2 biases of its feature tile and (16-row critic head) the value row
+    float bkres[kResW ? 16 : 1];
+    bf16x8 w3res[kResW && kCH16 ? 8 : 1];
+    float b3res = 0.0f;
+    if constexpr (kResW) {
+        const int h0 = (threadIdx.x & 63) >> 5;
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            bkres[q] = tanh_bias(((gf32*)p.b2)[(int64_t)(32 * ft0 + 8 * (q >> 2) + 4 * h0 + (q & 3)) * kHx]);
+        if constexpr (kCH16) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                w3res[k] = (lane & 15) == 0 ? *(const gbf16x8*)(p.W3rm + 32 * k + 8 * (lane >> 4)) : zero8();
+            b3res = ((gf32*)p.b3)[0];
+        }
+    }
     int64_t tile = blockIdx.x;
     if (tile < ntiles) fetch_x(tile);
     STAMP(15);
@@ -480,7 +519,12 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // the first W1 fragments go out before the barrier (their L2 latency overlaps its wait;
         // issued after the X stores, so they do not queue behind the X tile's HBM loads)
         WPre<kIn / 16> pw1;
-        w_prefetch(pw1, W1, kIn / 16, ft0, lane);
+        if constexpr (kResW) {
+#pragma unroll
+            for (int k = 0; k < kIn / 16; ++k) pw1.wf[k] = w1res[k];
+        } else {
+            w_prefetch(pw1, W1, kIn / 16, ft0, lane);
+        }
         STAMP(0);
         __syncthreads();
         STAMP(1);
@@ -497,7 +541,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         }
         // the first W2 fragments go out before the barrier (their L2 latency overlaps its wait)
         WPre<kH / 16> pw2;
-        w_prefetch(pw2, W2, kH / 16, ft0, lane);
+        if constexpr (!kResW) w_prefetch(pw2, W2, kH / 16, ft0, lane);
         STAMP(2);
         __syncthreads();
         STAMP(3);
@@ -555,7 +599,12 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             // (fwd_pipe measured 1 % slower here than the k-major chain + store_hidden)
 #if DXRL_L2_PIPE
             EpiTanh e2{H2, 32 * (ft0 + j) + 4 * h, r, bk};
-            fwd_pipe<kH / 16, kHp, kMT>(pw2, H1, lane, e2, l2_hook, (diag & 32) != 0);
+            if constexpr (kResW) {  // biases and head inputs resident: nothing to load
+                EpiTanh e2r{H2, 32 * (ft0 + j) + 4 * h, r, bkres};
+                fwd_pipe_w<kH / 16, kHp, kMT>(w2res, H1, lane, e2r, (diag & 32) != 0);
+            } else {
+                fwd_pipe<kH / 16, kHp, kMT>(pw2, H1, lane, e2, l2_hook, (diag & 32) != 0);
+            }
 #else
             f32x16 acc[kMT];
             fwd_run<kH / 16, kHp, kMT>(pw2, H1, acc, lane, l2_hook, (diag & 32) != 0);
@@ -584,7 +633,11 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
 #pragma unroll
             for (int k = 0; k < 8; ++k) w3h[k] = *(const gbf16x8*)(W3rm + 32 * k);
         }
-        if constexpr (kCH16) {
+        if constexpr (kCH16 && kResW) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w3h[k] = w3res[k];
+            b3h = b3res;
+        } else if constexpr (kCH16) {
             const bf16* W3rm = opaque(p.W3rm);
 #pragma unroll
             for (int k = 0; k < 8; ++k)

@@ -370,6 +370,15 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #ifndef DXRL_FWD_RESIDENT_W
 #define DXRL_FWD_RESIDENT_W 1
 #endif
+#ifndef DXRL_TRAIN_RESIDENT_W1
+#define DXRL_TRAIN_RESIDENT_W1 0
+#endif
+#ifndef DXRL_TRAIN_RESIDENT_HEAD
+#define DXRL_TRAIN_RESIDENT_HEAD 1
+#endif
+#ifndef DXRL_TRAIN_RESIDENT_B2
+#define DXRL_TRAIN_RESIDENT_B2 2
+#endif
 #ifndef DXRL_FUSED_PRIO
 #define DXRL_FUSED_PRIO 1
 #endif
@@ -471,25 +480,45 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     // whole launch (80 VGPRs; the train instantiations have no room for them) instead of streaming
     // 160 KB of weight fragments from L2 per tile and workgroup
     constexpr bool kResW = !kTrain && kNT == 1 && DXRL_FWD_RESIDENT_W && DXRL_L2_PIPE;
-    bf16x8 w1res[kResW ? kIn / 16 : 1], w2res[kResW ? kH / 16 : 1];
-    if constexpr (kResW) {
+    // (the train passes have room for the 16 registers of W1 only)
+    constexpr bool kResW1 = kNT == 1 && (kResW || (kTrain && DXRL_TRAIN_RESIDENT_W1));
+    bf16x8 w1res[kResW1 ? kIn / 16 : 1], w2res[kResW ? kH / 16 : 1];
+    if constexpr (kResW1) {
         const gbf16x8* p1 = (const gbf16x8*)p.W1 + (int64_t)ft0 * (kIn / 16) * 64 + lane;
-        const gbf16x8* p2 = (const gbf16x8*)p.W2 + (int64_t)ft0 * (kH / 16) * 64 + lane;
 #pragma unroll
         for (int k = 0; k < kIn / 16; ++k) w1res[k] = p1[64 * k];
+    }
+    if constexpr (kResW) {
+        const gbf16x8* p2 = (const gbf16x8*)p.W2 + (int64_t)ft0 * (kH / 16) * 64 + lane;
 #pragma unroll
         for (int k = 0; k < kH / 16; ++k) w2res[k] = p2[64 * k];
     }
     // ... and so do the layer-2 biases of its feature tile and (16-row critic head) the value row
-    float bkres[kResW ? 16 : 1];
-    bf16x8 w3res[kResW && kCH16 ? 8 : 1];
+    // (the critic's train pass has room for the biases, the actor's has not)
+    constexpr bool kResB = kNT == 1 && (kResW || (kTrain && (kNet == 1 || DXRL_TRAIN_RESIDENT_B2 > 1) && DXRL_TRAIN_RESIDENT_B2));
+    float bkres[kResB ? 16 : 1];
+    constexpr bool kResH = kCH16 && (kResW || (kTrain && DXRL_TRAIN_RESIDENT_HEAD));
+    bf16x8 w3res[kResH ? 8 : 1];
     float b3res = 0.0f;
-    if constexpr (kResW) {
+    // the actor head's per-lane constants (head rows 4 (lane >> 4) .. + 3): log sigma and mu bias
+    constexpr bool kResA = kAH16 && DXRL_TRAIN_RESIDENT_HEAD;
+    float ahls[kResA ? 4 : 1], ahb3[kResA ? 4 : 1];
+    if constexpr (kResA) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int o = 4 * (lane >> 4) + i;
+            ahls[i] = o < kAct ? ((gf32*)p.logstd)[o] : 0.0f;
+            ahb3[i] = ((gf32*)p.b3)[(int64_t)o * kHx];
+        }
+    }
+    if constexpr (kResB) {
         const int h0 = (threadIdx.x & 63) >> 5;
 #pragma unroll
         for (int q = 0; q < 16; ++q)
             bkres[q] = tanh_bias(((gf32*)p.b2)[(int64_t)(32 * ft0 + 8 * (q >> 2) + 4 * h0 + (q & 3)) * kHx]);
-        if constexpr (kCH16) {
+    }
+    if constexpr (kResH) {
+        {
 #pragma unroll
             for (int k = 0; k < 8; ++k)
                 w3res[k] = (lane & 15) == 0 ? *(const gbf16x8*)(p.W3rm + 32 * k + 8 * (lane >> 4)) : zero8();
@@ -519,7 +548,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // the first W1 fragments go out before the barrier (their L2 latency overlaps its wait;
         // issued after the X stores, so they do not queue behind the X tile's HBM loads)
         WPre<kIn / 16> pw1;
-        if constexpr (kResW) {
+        if constexpr (kResW1) {
 #pragma unroll
             for (int k = 0; k < kIn / 16; ++k) pw1.wf[k] = w1res[k];
         } else {
@@ -559,8 +588,10 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         auto head_inputs = [&]() {
             // the bias loads first: store_hidden waits for them, and must not wait for the HBM loads
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                bk[q] = tanh_bias(((gf32*)b2)[(int64_t)(32 * bft + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
+            for (int q = 0; q < 16; ++q) {
+                if constexpr (kResB) bk[q] = bkres[q];
+                else bk[q] = tanh_bias(((gf32*)b2)[(int64_t)(32 * bft + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
+            }
             if constexpr (kCH16) {
                 if (kTrain) {
                     const int64_t m16 = m0 + 16 * wave + (lane & 15);
@@ -633,7 +664,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
 #pragma unroll
             for (int k = 0; k < 8; ++k) w3h[k] = *(const gbf16x8*)(W3rm + 32 * k);
         }
-        if constexpr (kCH16 && kResW) {
+        if constexpr (kResH) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) w3h[k] = w3res[k];
             b3h = b3res;
@@ -703,9 +734,11 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int o = 4 * g4 + i;
-                lsv[i] = o < kAct ? ((gf32*)logstd)[o] : 0.0f;
+                if constexpr (kResA) lsv[i] = ahls[i];
+                else lsv[i] = o < kAct ? ((gf32*)logstd)[o] : 0.0f;
                 iv2[i] = __expf(-2.0f * lsv[i]);
-                mu[i] = a16[i] + ((gf32*)b3)[(int64_t)o * kHx];
+                if constexpr (kResA) mu[i] = a16[i] + ahb3[i];
+                else mu[i] = a16[i] + ((gf32*)b3)[(int64_t)o * kHx];
                 const float z = (a[i] - mu[i]) * __expf(-lsv[i]);
                 t[i] = o < kAct ? -0.5f * z * z - lsv[i] - 0.5f * kLog2PiF : 0.0f;
                 d[i] = 0.0f;

@@ -942,6 +942,9 @@ struct WsReward {      // an env's dense-reward inputs and episode end of one st
 // kNoise: configs with fused noise (or the noise parity tapes); kDiag: diag_flags / parity tapes
 // set.  The production instantiations compile out every runtime check of the other's features
 // (branches and SGPRs inside the step loop: -8 % rollout time for <false, false>).
+#ifndef DXRL_WS_PRIO
+#define DXRL_WS_PRIO -1  // -1: by instantiation (env waves first with fused noise)
+#endif
 template <bool kNoise, bool kDiag>
 __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p) {
     constexpr int kRows = 32;
@@ -964,6 +967,13 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     __shared__ uint32_t KEYS[kLsEnvs][4];           // per env: reset key ek0, ek1, policy key pk0, pk1
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool aux = wave >= 4;
+    // waves w and w + 4 share SIMD w; with fused noise the env waves issue first (P0's aux lanes
+    // run a Philox round beside the observation row): noise configs -2.2 % rollout, the others
+    // +1 % (so they keep equal priorities); aux first or per-phase priorities lose 5-10 %
+    // (rollout_time A/B, profiles/r04/ab_rollout_wave_priority.log)
+    constexpr int kPrio = DXRL_WS_PRIO >= 0 ? DXRL_WS_PRIO : (kNoise ? 1 : 0);
+    if (kPrio != 0 && (__builtin_amdgcn_readfirstlane(wave) >= 4) == (kPrio == 2))
+        __builtin_amdgcn_s_setprio(1);
     const int et_tid = tid & 255;  // the env lane this thread is (env wave) or twins (aux wave)
     const int eg = et_tid >> 4, s = et_tid & 15, gbit = 16 * (eg & 3);
     const int rbase = et_tid & ~15;

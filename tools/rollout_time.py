@@ -1,4 +1,5 @@
-"""Time the fused PG rollout kernels (ws default, ls = diag 64) at the bench shape, one line."""
+"""Time the fused PG rollout kernels (ws default, ls = diag 64; ONE=1 adds the one-lane-per-env
+kernel, diag 16) at the bench shape (ENVS, default 4096), one line."""
 import os
 import sys
 
@@ -12,10 +13,11 @@ dev = torch.device("cuda:0")
 cur = os.environ.get("CUR", "easy")
 out = []
 for noise in (0.0, 0.05):
-    env = envs.VecEnv(4096, curriculum_config=pkg.CurriculumConfig.named(cur), reward_type="dense", seed=1, device=dev)
+    env = envs.VecEnv(int(os.environ.get("ENVS", "4096")), curriculum_config=pkg.CurriculumConfig.named(cur), reward_type="dense", seed=1, device=dev)
     tr = trainer.PGTrainer(env, trainer.TrainerConfig(horizon=200, seed=7, obs_noise_std=noise, dyn_noise_std=noise))
     env.reset(write_obs=False)
-    for flags, name in ((0, "ws"), (64, "ls")):
+    kernels = ((0, "ws"), (64, "ls")) + (((16, "one"),) if os.environ.get("ONE") else ())
+    for flags, name in kernels:
         tr.diag_flags = flags
         tr.rollout()
         torch.cuda.synchronize()

@@ -47,39 +47,63 @@ struct Tri {
 };
 __device__ __forceinline__ Tri add(Tri a, Tri b) { return Tri{a.c + b.c, a.s + b.s, a.u + b.u}; }
 
-// exclusive scan of one Tri per thread over a workgroup (Hillis-Steele in LDS)
+// exclusive scan of one Tri per thread over a workgroup: inclusive scans of the 64-lane waves by
+// shuffles, then the wave totals through LDS (lds: >= NT / 64 entries; integer sums, so any
+// association gives the same result).  Ends with a barrier: lds is free again on return.
 template <int NT>
 __device__ Tri block_exclusive_scan(Tri v, Tri* lds, Tri& total) {
-    const int tid = threadIdx.x;
-    lds[tid] = v;
-    __syncthreads();
-    for (int d = 1; d < NT; d <<= 1) {
-        Tri o{0, 0, 0};
-        if (tid >= d) o = lds[tid - d];
-        __syncthreads();
-        if (tid >= d) lds[tid] = add(lds[tid], o);
-        __syncthreads();
+    static_assert(NT % 64 == 0 && NT <= 4096, "whole waves");
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    Tri inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const Tri o{__shfl_up(inc.c, d), __shfl_up(inc.s, d), __shfl_up(inc.u, d)};
+        if (lane >= d) inc = add(inc, o);
     }
-    total = lds[NT - 1];
-    Tri ex = tid ? lds[tid - 1] : Tri{0, 0, 0};
+    if (lane == 63) lds[w] = inc;
     __syncthreads();
-    return ex;
+    Tri pre{0, 0, 0}, tot{0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k) {
+        const Tri s = lds[k];
+        if (k < w) pre = add(pre, s);
+        tot = add(tot, s);
+    }
+    total = tot;
+    __syncthreads();
+    return Tri{pre.c + inc.c - v.c, pre.s + inc.s - v.s, pre.u + inc.u - v.u};
+}
+
+// the kPer codes g0 .. g0 + kPer - 1 (0 past the end): one 16-byte load when the view is one
+// contiguous rank (the order (t, r, i) is then the buffer's own) and the run is aligned
+__device__ __forceinline__ void load_codes(const CodeView& v, int64_t g0, uint16_t (&x)[kPer]) {
+    static_assert(kPer == 8, "one 16-byte load");
+    if (v.world == 1 && g0 + kPer <= v.L && ((reinterpret_cast<uintptr_t>(v.codes) & 15) == 0)) {
+        const uint4 q = *reinterpret_cast<const uint4*>(v.codes + g0);  // g0 % 8 == 0
+        const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            x[2 * k] = (uint16_t)(w4[k] & 0xFFFFu);
+            x[2 * k + 1] = (uint16_t)(w4[k] >> 16);
+        }
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) x[k] = g0 + k < v.L ? v.at(g0 + k) : (uint16_t)0;
 }
 
 __global__ __launch_bounds__(kThreads) void k_sched_count(CodeView v, Tri* blk) {
     __shared__ Tri lds[kThreads];
     const int64_t g0 = (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kPer;
+    uint16_t x[kPer];
+    load_codes(v, g0, x);
     Tri a{0, 0, 0};
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int64_t g = g0 + k;
-        if (g < v.L) {
-            const uint16_t x = v.at(g);
-            if (x) {
-                a.c += 1;
-                a.s += x >> 1;
-                a.u += x & 1;
-            }
+        if (x[k]) {
+            a.c += 1;
+            a.s += x[k] >> 1;
+            a.u += x[k] & 1;
         }
     }
     Tri tot;
@@ -121,11 +145,10 @@ __global__ __launch_bounds__(kThreads) void k_sched_scatter(CodeView v, const Tr
     __shared__ Tri lds[kThreads];
     const int64_t g0 = (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kPer;
     uint16_t x[kPer];
+    load_codes(v, g0, x);
     Tri a{0, 0, 0};
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int64_t g = g0 + k;
-        x[k] = g < v.L ? v.at(g) : (uint16_t)0;
         if (x[k]) {
             a.c += 1;
             a.s += x[k] >> 1;
@@ -274,21 +297,26 @@ __host__ __device__ inline PackLayout pack_layout(int64_t T, int64_t N, int32_t 
 }
 
 template <typename V>
-__device__ V block_exclusive_scan_v(V v, V* lds, V& total) {
-    const int tid = threadIdx.x;
-    lds[tid] = v;
-    __syncthreads();
-    for (int d = 1; d < kThreads; d <<= 1) {
-        V o{};
-        if (tid >= d) o = lds[tid - d];
-        __syncthreads();
-        if (tid >= d) lds[tid] = lds[tid] + o;
-        __syncthreads();
+__device__ V block_exclusive_scan_v(V v, V* lds, V& total) {  // as block_exclusive_scan, one value
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    V inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const V o = __shfl_up(inc, d);
+        if (lane >= d) inc = inc + o;
     }
-    total = lds[kThreads - 1];
-    V ex = tid ? lds[tid - 1] : V{};
+    if (lane == 63) lds[w] = inc;
     __syncthreads();
-    return ex;
+    V pre{}, tot{};
+#pragma unroll
+    for (int k = 0; k < kThreads / 64; ++k) {
+        const V s = lds[k];
+        if (k < w) pre = pre + s;
+        tot = tot + s;
+    }
+    total = tot;
+    __syncthreads();
+    return pre + inc - v;
 }
 
 // one workgroup per step: this rank's (episodes, steps, successes) ending at t

@@ -463,10 +463,23 @@ class PGTrainer:
         self.codes_all = self.ep_code if not self.collective else None  # host mode's all-gather (lazy)
         w = max(1, int(scheduler.window_size))
         self._sched_w = w
-        self._tail_dev = torch.zeros(2, w, dtype=torch.int16, device=d)
-        self._tail_len_dev = torch.zeros(2, dtype=torch.int32, device=d)
-        self._tail_in_host = torch.zeros(w, dtype=torch.int16).pin_memory()
-        self._tail_len_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        # one staging block each way, so a feed is one H2D and one D2H copy (each small copy is a
+        # ~5 us blit on the stream): in = [tail_len i32][tail i16 x w]; out = [summary i64 x S]
+        # [tail_len i32][tail i16 x w]
+        S = 4 + 3 * N.SCHED_MAX_CANDIDATES
+        self._sched_in_host = torch.zeros(4 + 2 * w, dtype=torch.uint8).pin_memory()
+        self._sched_in_dev = torch.zeros(4 + 2 * w, dtype=torch.uint8, device=d)
+        self._sched_out_dev = torch.zeros(8 * S + 4 + 2 * w, dtype=torch.uint8, device=d)
+        self._sched_out_host = torch.zeros(8 * S + 4 + 2 * w, dtype=torch.uint8).pin_memory()
+        self._tail_len_host = self._sched_in_host[:4].view(torch.int32)
+        self._tail_in_host = self._sched_in_host[4:].view(torch.int16)
+        self._tail_len_in_dev = self._sched_in_dev[:4].view(torch.int32)
+        self._tail_in_dev = self._sched_in_dev[4:].view(torch.int16)
+        self._summary = self._sched_out_dev[:8 * S].view(torch.int64)
+        self._tail_len_out_dev = self._sched_out_dev[8 * S:8 * S + 4].view(torch.int32)
+        self._tail_out_dev = self._sched_out_dev[8 * S + 4:].view(torch.int16)
+        self._summary_host = self._sched_out_host[:8 * S].view(torch.int64)
+        self._tail_out_host = self._sched_out_host[8 * S + 4:].view(torch.int16)
         nb = C.c_int64()
         # sharded: the packed exchange (dxrl_sched_pack holds a step's episode steps in u32)
         self._packed = self.collective and n < (1 << 18)
@@ -483,9 +496,6 @@ class PGTrainer:
         else:
             N.call("dxrl_sched_scratch_bytes", 1, T, n, w, C.byref(nb))
         self._sched_scratch = torch.empty(nb.value, dtype=torch.uint8, device=d)
-        self._summary = torch.zeros(4 + 3 * N.SCHED_MAX_CANDIDATES, dtype=torch.int64, device=d)
-        self._summary_host = torch.zeros_like(self._summary, device="cpu").pin_memory()
-        self._tail_out_host = torch.zeros(w, dtype=torch.int16).pin_memory()
         self._codes_host = None
         self._sched_event = torch.cuda.Event()
         self._sched_mode = None
@@ -511,13 +521,12 @@ class PGTrainer:
             self._tail_len_host[0] = len(tail)
             if tail:
                 self._tail_in_host[:len(tail)] = torch.tensor(tail, dtype=torch.int16)
-            self._tail_dev[0].copy_(self._tail_in_host, non_blocking=True)
-            self._tail_len_dev[0:1].copy_(self._tail_len_host, non_blocking=True)
+            self._sched_in_dev.copy_(self._sched_in_host, non_blocking=True)
             a = N.SchedPackedArgs() if self.collective else N.SchedArgs()
             a.window, a.max_candidates, a.threshold = w, P, float(sc.success_rate_threshold)
             a.min_episodes, a.episodes_before = int(sc.min_episodes_before_progression), int(sc.total_episodes)
-            a.tail_in, a.tail_len_in = N.ptr(self._tail_dev[0]), N.ptr(self._tail_len_dev[0:1])
-            a.tail_out, a.tail_len_out = N.ptr(self._tail_dev[1]), N.ptr(self._tail_len_dev[1:2])
+            a.tail_in, a.tail_len_in = N.ptr(self._tail_in_dev), N.ptr(self._tail_len_in_dev)
+            a.tail_out, a.tail_len_out = N.ptr(self._tail_out_dev), N.ptr(self._tail_len_out_dev)
             a.scratch, a.scratch_bytes, a.summary = N.ptr(self._sched_scratch), self._sched_scratch.numel(), \
                 N.ptr(self._summary)
             a.world, a.horizon, a.num_envs = self.world, self.T, self.n
@@ -526,8 +535,7 @@ class PGTrainer:
                 N.call("dxrl_sched_scan", self.dev.index, C.byref(a), self._s())
             else:
                 self._packed_feed(a, P)
-            self._summary_host.copy_(self._summary, non_blocking=True)
-            self._tail_out_host.copy_(self._tail_dev[1], non_blocking=True)
+            self._sched_out_host.copy_(self._sched_out_dev, non_blocking=True)
             self._sched_mode = "device"
         else:
             if self.codes_all is None:

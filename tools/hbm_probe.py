@@ -1,9 +1,9 @@
-"""HBM ceilings on this box for the k_step mix: read-only, write-only, copy (torch kernels), 2.5 GB."""
+"""HBM ceilings on this box (torch kernels over 671 MB buffers): read-only, write-only, copy, axpy."""
 import torch
 
 dev = torch.device("cuda:0")
-n = 640 * 1024 * 1024 // 4 * 4  # 2.5 GiB of f32
-a = torch.empty(n // 4, dtype=torch.float32, device=dev).uniform_()
+n = 640 * 1024 * 1024 // 4  # 671 MB of f32 per buffer (well past the 256 MB Infinity Cache)
+a = torch.empty(n, dtype=torch.float32, device=dev).uniform_()
 b = torch.empty_like(a)
 
 
@@ -23,4 +23,4 @@ nb = a.numel() * 4
 for name, fn, byts in [("read (sum)", lambda: a.sum(), nb), ("write (fill)", lambda: b.fill_(1.0), nb),
                        ("copy", lambda: b.copy_(a), 2 * nb), ("axpy-like (b=a*2)", lambda: torch.mul(a, 2.0, out=b), 2 * nb)]:
     ms = t(fn)
-    print(f"{name:20s} {ms:.3f} ms {byts / ms / 1e9:.0f} GB/s")
+    print(f"{name:20s} {ms:.3f} ms {byts / ms / 1e9:.2f} TB/s")

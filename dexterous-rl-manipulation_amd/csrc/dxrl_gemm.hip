@@ -773,6 +773,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
     }
     float* dst = w.partial ? w.partial + (int64_t)blockIdx.x * 256 * 256 : w.out;
     const int64_t ld = w.partial ? 256 : w.ldo;
+    if (kDiag && (w.diag & 4)) return;  // ablation: no partial-slab stores
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int i = 32 * j + (lane & 31);

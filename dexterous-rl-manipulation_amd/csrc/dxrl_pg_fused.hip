@@ -370,14 +370,14 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #ifndef DXRL_FWD_RESIDENT_W
 #define DXRL_FWD_RESIDENT_W 1
 #endif
-#ifndef DXRL_TRAIN_RESIDENT_W1
-#define DXRL_TRAIN_RESIDENT_W1 0
-#endif
 #ifndef DXRL_TRAIN_RESIDENT_HEAD
 #define DXRL_TRAIN_RESIDENT_HEAD 1
 #endif
+// the train passes' layer-2 biases and (DXRL_TRAIN_RESIDENT_HEAD) the heads' constants in
+// registers for the launch: actor 400 -> 384 us, critic 377 -> 363 us (kernel-level A/B,
+// profiles/r04/ab_kernels_train_resident_consts.log); W1's 16 registers as well: no change
 #ifndef DXRL_TRAIN_RESIDENT_B2
-#define DXRL_TRAIN_RESIDENT_B2 2
+#define DXRL_TRAIN_RESIDENT_B2 1
 #endif
 #ifndef DXRL_FUSED_PRIO
 #define DXRL_FUSED_PRIO 1
@@ -480,22 +480,18 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     // whole launch (80 VGPRs; the train instantiations have no room for them) instead of streaming
     // 160 KB of weight fragments from L2 per tile and workgroup
     constexpr bool kResW = !kTrain && kNT == 1 && DXRL_FWD_RESIDENT_W && DXRL_L2_PIPE;
-    // (the train passes have room for the 16 registers of W1 only)
-    constexpr bool kResW1 = kNT == 1 && (kResW || (kTrain && DXRL_TRAIN_RESIDENT_W1));
-    bf16x8 w1res[kResW1 ? kIn / 16 : 1], w2res[kResW ? kH / 16 : 1];
-    if constexpr (kResW1) {
+    bf16x8 w1res[kResW ? kIn / 16 : 1], w2res[kResW ? kH / 16 : 1];
+    if constexpr (kResW) {
         const gbf16x8* p1 = (const gbf16x8*)p.W1 + (int64_t)ft0 * (kIn / 16) * 64 + lane;
 #pragma unroll
         for (int k = 0; k < kIn / 16; ++k) w1res[k] = p1[64 * k];
-    }
-    if constexpr (kResW) {
         const gbf16x8* p2 = (const gbf16x8*)p.W2 + (int64_t)ft0 * (kH / 16) * 64 + lane;
 #pragma unroll
         for (int k = 0; k < kH / 16; ++k) w2res[k] = p2[64 * k];
     }
     // ... and so do the layer-2 biases of its feature tile and (16-row critic head) the value row
-    // (the critic's train pass has room for the biases, the actor's has not)
-    constexpr bool kResB = kNT == 1 && (kResW || (kTrain && (kNet == 1 || DXRL_TRAIN_RESIDENT_B2 > 1) && DXRL_TRAIN_RESIDENT_B2));
+    // (the train passes too: the biases fit beside their accumulators, W2 / W2T do not)
+    constexpr bool kResB = kNT == 1 && (kResW || (kTrain && DXRL_TRAIN_RESIDENT_B2));
     float bkres[kResB ? 16 : 1];
     constexpr bool kResH = kCH16 && (kResW || (kTrain && DXRL_TRAIN_RESIDENT_HEAD));
     bf16x8 w3res[kResH ? 8 : 1];
@@ -548,7 +544,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // the first W1 fragments go out before the barrier (their L2 latency overlaps its wait;
         // issued after the X stores, so they do not queue behind the X tile's HBM loads)
         WPre<kIn / 16> pw1;
-        if constexpr (kResW1) {
+        if constexpr (kResW) {
 #pragma unroll
             for (int k = 0; k < kIn / 16; ++k) pw1.wf[k] = w1res[k];
         } else {

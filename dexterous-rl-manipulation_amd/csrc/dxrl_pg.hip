@@ -1590,7 +1590,18 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(const float* __restrict__ r
 //   3. all 256 threads write adv / ret back coalesced and accumulate the moments.
 // k_gae (64 single-wave workgroups, the whole step on the chain, a memory latency per 32-step
 // chunk) remains for horizons whose staging exceeds the LDS.
+#ifndef DXRL_GAE_XCD
+#define DXRL_GAE_XCD 1
+#endif
 constexpr int kGlEnvs = 16, kGlThreads = 256;
+// Workgroups are dispatched to the 8 XCDs round robin (block b on XCD b % 8): env group g of
+// block b chosen so each XCD owns one contiguous run of groups, and the 64-byte row pieces of
+// neighbouring groups (one 128-byte line) are fetched into one L2, not two.  A permutation of
+// the groups for any dispatch order; partial[] stays indexed by group, so every sum is unchanged.
+__device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t nb) {
+    const int64_t q = nb / 8, rem = nb % 8, x = b % 8, j = b / 8;
+    return x * q + (x < rem ? x : rem) + j;
+}
 __host__ __device__ constexpr int64_t gae_lds_bytes(int64_t T) { return T * kGlEnvs * 13; }
 __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict__ rew,
                                                         const uint8_t* __restrict__ done, const float* __restrict__ V,
@@ -1604,7 +1615,8 @@ __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict_
     uint8_t* Ds = reinterpret_cast<uint8_t*>(As + (int64_t)T * kGlEnvs);  // [T][16] done
     __shared__ Moments red[kGlThreads];
     const int tid = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * kGlEnvs;
+    const int64_t grp = DXRL_GAE_XCD ? xcd_contiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t e0 = grp * kGlEnvs;
     const int64_t cnt = (int64_t)T * kGlEnvs;
     // 1. batches of kGlBatch elements per thread, every load issued before any lands
     constexpr int kGlBatch = 16;
@@ -1693,7 +1705,7 @@ __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict_
     }
     const Moments mo = c > 0.0 ? Moments{c, K + s / c, fmax(s2 - s * (s / c), 0.0)} : Moments{0.0, 0.0, 0.0};
     block_merge<kGlThreads>(mo, red);
-    if (tid == 0) partial[blockIdx.x] = red[0];
+    if (tid == 0) partial[grp] = red[0];
 }
 
 // Local moments of the rank, contiguous so ranks exchange them as one 3-element block:

@@ -57,10 +57,16 @@ struct TileLds {
 };
 
 // per-workgroup gradient partial slab (f32)
-constexpr int kPartW1 = 0;                   // [256][64]
-constexpr int kPartW3 = kPartW1 + kH * kIn;  // [32][288]
-constexpr int kPartLs = kPartW3 + kOut * kHx;
-constexpr int kPartB2 = kPartLs + 16;        // [256]: dL/db2 column sums
+// Workgroup partial slab: only what a pass can make nonzero -- dW1 input columns 0..47 (45
+// observation features + the bias column; X is zero beyond), dW3 head rows 0..15 (15 mu rows /
+// the value row) with their bias column, padded to a float4 multiple; the scatter writes the
+// zeros of the rest of the grads blocks
+constexpr int kPW1C = 48;                        // dW1 columns kept
+constexpr int kPW3C = kH + 4;                    // dW3 columns kept: 0..255, bias 256, pad 257..259
+constexpr int kPartW1 = 0;                       // [256][48]
+constexpr int kPartW3 = kPartW1 + kH * kPW1C;    // [16][260]
+constexpr int kPartLs = kPartW3 + 16 * kPW3C;
+constexpr int kPartB2 = kPartLs + 16;            // [256]: dL/db2 column sums
 constexpr int kPartSize = kPartB2 + kH;
 
 // global-address-space views: loads through them compile to global_load (vmcnt only); a
@@ -1043,13 +1049,12 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             for (int i = 0; i < 4; ++i) {
                 const int o = 4 * g16 + i;  // head row (rows 16..31 stay zero: k_fused_scatter)
 #pragma unroll
-                for (int ci = 0; ci < 2; ++ci) part[kPartW3 + o * kHx + 32 * (ft0 + j) + 16 * ci + c16] = acc3[j][ci][i];
+                for (int ci = 0; ci < 2; ++ci) part[kPartW3 + o * kPW3C + 32 * (ft0 + j) + 16 * ci + c16] = acc3[j][ci][i];
 #pragma unroll
                 for (int ri = 0; ri < 2; ++ri) {
-                    float* row = part + kPartW1 + (32 * (ft0 + j) + 16 * ri + o) * kIn;
+                    float* row = part + kPartW1 + (32 * (ft0 + j) + 16 * ri + o) * kPW1C;
 #pragma unroll
                     for (int ci = 0; ci < 3; ++ci) row[16 * ci + c16] = acc1[j][ri][ci][i];
-                    row[48 + c16] = 0.0f;  // input columns 48..63: X is zero there
                 }
             }
     }
@@ -1067,8 +1072,10 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             if (tid == 0)
                 for (int w = 0; w < kFW; ++w)
                     for (int rr = 0; rr < 16; ++rr) sb += red[64 * w + rr];
-            part[kPartW3 + tid * kHx + kH] = sb;  // bias column of head row tid (rows > 0: zero)
-            if (tid < 16) part[kPartLs + tid] = 0.0f;
+            if (tid < 16) {
+                part[kPartW3 + tid * kPW3C + kH] = sb;  // bias column of head row tid (rows > 0: zero)
+                part[kPartLs + tid] = 0.0f;
+            }
         } else if (tid == 33) {
             double s = 0.0;
             for (int w = 0; w < kFW; ++w)
@@ -1102,8 +1109,10 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                         sb += red[t * 8 + 4 + i];
                     }
             }
-            part[kPartW3 + o * kHx + kH] = sb;  // bias column of the head
-            if (o < 16) part[kPartLs + o] = sl;
+            if (o < 16) {
+                part[kPartW3 + o * kPW3C + kH] = sb;  // bias column of the head
+                part[kPartLs + o] = sl;
+            }
         } else if (tid < 36) {
             const int k = tid - 32;
             if (k != 1) {
@@ -1138,8 +1147,10 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                     sb += red[t * 16 + 8 + q];
                 }
         }
-        part[kPartW3 + o * kHx + kH] = sb;  // bias column of the head
-        if (o < 16) part[kPartLs + o] = sl;
+        if (o < 16) {
+            part[kPartW3 + o * kPW3C + kH] = sb;  // bias column of the head
+            part[kPartLs + o] = sl;
+        }
     } else if (tid < 36) {
         const int k = tid - 32;
         double s = 0.0;
@@ -1165,13 +1176,24 @@ __device__ __forceinline__ void fused_scatter_one(int j, float s, float* __restr
         }
         return;
     }
-    const int col = (j - kPartW3) % kHx, orow = (j - kPartW3) / kHx;
-    // never written by k_pg_fused: the pad columns 257.. and the dW3 rows 16..31 but their bias column
-    const bool w3pad = j >= kPartW3 && j < kPartLs && (col > kH || (orow >= 16 && col < kH));
-    if (w3pad) s = 0.0f;
-    if (j < kPartW3) gW1[j] = s;
-    else if (j < kPartLs) gW3[j - kPartW3] = s;
-    else if (gLs) {
+    if (j < kPartW3) {  // dW1 [256][64]: columns 0..47 from the slab, 48..63 zero
+        const int row = j / kPW1C, col = j % kPW1C;
+        gW1[row * kIn + col] = s;
+        if (col < kIn - kPW1C) gW1[row * kIn + kPW1C + col] = 0.0f;
+        return;
+    }
+    if (j < kPartLs) {  // dW3 [32][288]: rows 0..15 columns 0..256 from the slab, the rest zero
+        const int o = (j - kPartW3) / kPW3C, col = (j - kPartW3) % kPW3C;
+        if (col <= kH) gW3[o * kHx + col] = s;
+        if (col < kH) {
+            gW3[(16 + o) * kHx + col] = 0.0f;  // rows 16..31
+        } else if (col == kH) {  // row o's pad columns 257..287, row 16 + o's columns 256..287
+            for (int c = kH + 1; c < kHx; ++c) gW3[o * kHx + c] = 0.0f;
+            for (int c = kH; c < kHx; ++c) gW3[(16 + o) * kHx + c] = 0.0f;
+        }
+        return;
+    }
+    if (gLs) {
         const int k = j - kPartLs;
         gLs[k] = k < kAct ? s - ent_coef : 0.0f;
     }

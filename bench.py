@@ -60,6 +60,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--prewarm-s", type=float, default=1.0,
+                   help="untimed iterations for at least this long before the --warmup ones: the GPU's clocks "
+                        "take the first ~0.1-1 s of work to reach their sustained level (DESIGN.md §6)")
     p.add_argument("--config", choices=sorted(WORKLOADS), default="easy",
                    help="BASELINE configs[1..4]: easy (C2, the metric's config), default (C3: curriculum "
                         "scheduler), hard_heldout (C4: held-out object table, 8192 envs), variable_noise (C5)")
@@ -81,6 +84,8 @@ def parse():
     p.add_argument("--sched-restart", action="store_true",
                    help="C3: restart the CurriculumScheduler from its initial config at the start of every "
                         "iteration (CurriculumScheduler.reset()), so every timed iteration replays progressions")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="collectives on the compute stream (TrainerConfig.overlap_comm=False)")
     p.add_argument("--dist", action="store_true",
                    help="create the RCCL process group even at --gpus 1 (before any GPU work) and run the "
                         "multi-rank code path: the trainer's collectives, barrier and max-over-ranks timing")
@@ -172,6 +177,8 @@ def pg_bench(args, world, rank, dev):
         import torch.distributed as dist
         pg = dist.group.WORLD
     kw = {"success_rule": args.success_rule} if args.success_rule else {}
+    if args.no_overlap:
+        kw["overlap_comm"] = False
     env, tr = build_pg_workload(args.config, dev, rank=rank, world=world, process_group=pg, envs=args.envs,
                                 horizon=args.horizon, curriculum=args.curriculum, epochs=args.epochs,
                                 minibatches=args.minibatches, **kw)
@@ -185,6 +192,16 @@ def pg_bench(args, world, rank, dev):
             env.set_curriculum_async(sc.get_current_config())
         tr.iteration()
 
+    # bring the GPU to its sustained clock first (not part of the W warmup steps or the timed K):
+    # blocks of 8 iterations until the slowest rank has run for prewarm_s (every rank runs the
+    # same number of iterations, so their collectives pair up)
+    prewarm_iters, tp, prewarm_s = 0, time.perf_counter(), 0.0
+    while prewarm_s < args.prewarm_s:
+        for _ in range(8):
+            one_iteration()
+        torch.cuda.synchronize(dev)
+        prewarm_iters += 8
+        prewarm_s = max_over_ranks(time.perf_counter() - tp, world, dev)
     for _ in range(args.warmup):
         one_iteration()
     torch.cuda.synchronize(dev)
@@ -230,6 +247,7 @@ def pg_bench(args, world, rank, dev):
         stats["scheduler_episodes"] = int(tr.scheduler.total_episodes)
         stats["progressions_applied_in_timed_iterations"] = prog_timed
         stats["success_rule"] = tr.cfg.success_rule
+    stats["prewarm"] = {"s": round(prewarm_s, 3), "iterations": prewarm_iters}
     stats.update({k: round(v, 5) for k, v in tr.loss_stats().items()})
     return wall, phases, mfma, stats
 

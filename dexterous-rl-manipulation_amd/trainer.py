@@ -82,7 +82,12 @@ class TrainerConfig:
     minibatches: int = 1                     # time-contiguous minibatches per epoch, order shuffled per epoch
                                              # (1 x 1: one update, ratio == 1 -- an A2C-style step)
     success_rule: str = "terminated"         # "training" (episode_utils.py:52) or "terminated"
-    overlap_comm: bool = True                # collectives on a side stream, overlapped with the train passes
+    # collectives on a side stream beside the train passes (True) or on the compute stream between
+    # them (False, default): the learner kernels are persistent and fill every CU, so a collective
+    # beside them delays them by about its own length and the cross-stream ordering adds the rest;
+    # at world 1 over RCCL the overlapped form costs 85 us per iteration, the serialised one 31 us
+    # (profiles/r04/ab_dist_overlap.log).  Both give bit-identical results.
+    overlap_comm: bool = False
 
 
 def minibatch_bounds(M: int, B: int, round_samples: int):

@@ -6,8 +6,8 @@ advantage-moment triple, the all-gather of the u16 episode codes as bytes, the i
 global_count SUM and the f64 MAX.  Each must return its input; and a PGTrainer driven
 through that group (3 full iterations, curriculum-scheduler and fused-noise configs) must
 give the group-less trainer's gradients, statistics, episode codes and parameters bit for
-bit -- with its exchanges on the side stream overlapping the train passes (the default) and
-serialised on the compute stream (overlap_comm=False).  Multi-rank semantics are covered by tests/test_dist_gloo.py (CPU) and
+bit -- with its exchanges on the side stream overlapping the train passes (overlap_comm=True) and
+serialised on the compute stream (overlap_comm=False, the default).  Multi-rank semantics are covered by tests/test_dist_gloo.py (CPU) and
 tests/test_gpu_dist.py (two ranks on one GPU over gloo)."""
 import os
 import socket

@@ -5,6 +5,10 @@
 //   reg   every wave loads its 2.5 KiB of the chunk into registers (global_load_dwordx4), the same
 //         barrier per chunk, values folded into one XOR so nothing is dead
 //   regnb the same without barriers
+//   dma2  as dma, but from two buffers like k_wgrad_l1's sources: 16 KB of dH2 rows and 4 KB of
+//         observation rows per chunk (four pieces from the first, one from the second per wave)
+//   dma2w dma2 right after the whole buffer was rewritten (as dH2 is by the pass before
+//         k_wgrad_l1: dirty lines in the caches when the stream starts)
 // hipcc --offload-arch=gfx950 -O3 tools/stream_mb.hip -o tools/stream_mb && ./tools/stream_mb
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,14 +26,27 @@ __device__ __forceinline__ void glds_x4(const void* src, const void* lds_dst) {
                  : "memory");
 }
 
+template <bool kTwo>
 __global__ __launch_bounds__(kThreads, 1) void k_dma(const char* src, int64_t nchunks, uint32_t* out) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nch = (int)((nchunks - blockIdx.x + gridDim.x - 1) / gridDim.x);
     const auto issue = [&](int c) {
         if (wave >= 4) return;
-        const char* base = src + ((int64_t)blockIdx.x + (int64_t)c * gridDim.x) * kChunk;
+        const int64_t g = (int64_t)blockIdx.x + (int64_t)c * gridDim.x;
         char* slot = lds + (c % kRing) * kChunk;
+        if (kTwo) {
+            const char* y = src + g * 16384;
+            const char* x = src + nchunks * 16384 + g * 4096;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int piece = 4 * wave + i;
+                glds_x4(y + piece * 1024 + 16 * lane, slot + piece * 1024);
+            }
+            glds_x4(x + wave * 1024 + 16 * lane, slot + 16384 + wave * 1024);
+            return;
+        }
+        const char* base = src + g * kChunk;
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
             const int piece = 5 * wave + i;  // 20 pieces of 1 KiB
@@ -81,24 +98,30 @@ int main() {
     uint32_t* out;
     if (hipMalloc(&src, nchunks * kChunk) != hipSuccess || hipMalloc(&out, kGrid * kThreads * 4) != hipSuccess) return 1;
     hipMemset(src, 1, nchunks * kChunk);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(k_dma), hipFuncAttributeMaxDynamicSharedMemorySize, kRing * kChunk);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(k_dma<false>), hipFuncAttributeMaxDynamicSharedMemorySize, kRing * kChunk);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(k_dma<true>), hipFuncAttributeMaxDynamicSharedMemorySize, kRing * kChunk);
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    for (int v = 0; v < 3; ++v) {
+    for (int v = 0; v < 5; ++v) {
         float best = 1e9f;
         for (int rep = 0; rep < 6; ++rep) {
+            if (v == 4) {
+                hipMemsetAsync(src, rep, nchunks * kChunk);
+                hipDeviceSynchronize();
+            }
             hipEventRecord(a);
-            if (v == 0) hipLaunchKernelGGL(k_dma, dim3(kGrid), dim3(kThreads), kRing * kChunk, 0, src, nchunks, out);
+            if (v == 0) hipLaunchKernelGGL(k_dma<false>, dim3(kGrid), dim3(kThreads), kRing * kChunk, 0, src, nchunks, out);
             if (v == 1) hipLaunchKernelGGL(k_reg<true>, dim3(kGrid), dim3(kThreads), 0, 0, src, nchunks, out);
             if (v == 2) hipLaunchKernelGGL(k_reg<false>, dim3(kGrid), dim3(kThreads), 0, 0, src, nchunks, out);
+            if (v >= 3) hipLaunchKernelGGL(k_dma<true>, dim3(kGrid), dim3(kThreads), kRing * kChunk, 0, src, nchunks, out);
             hipEventRecord(b);
             hipEventSynchronize(b);
             float ms;
             hipEventElapsedTime(&ms, a, b);
             if (rep && ms < best) best = ms;
         }
-        printf("%-6s %8.1f us  %.2f TB/s\n", v == 0 ? "dma" : v == 1 ? "reg" : "regnb", best * 1e3,
+        printf("%-6s %8.1f us  %.2f TB/s\n", v == 0 ? "dma" : v == 1 ? "reg" : v == 2 ? "regnb" : v == 3 ? "dma2" : "dma2w", best * 1e3,
                (double)nchunks * kChunk / (best * 1e-3) / 1e12);
     }
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;

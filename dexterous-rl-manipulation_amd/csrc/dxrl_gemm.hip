@@ -948,6 +948,7 @@ int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, 
     DXRL_REQUIRE((reinterpret_cast<uintptr_t>(Y) & 15) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0,
                  "wgrad: operands must be 16-byte aligned");
     if (splits < 1) splits = 1;
+    const int requested = splits;
     int64_t chunk = (M + splits - 1) / splits;
     chunk = (chunk + kWK - 1) / kWK * kWK;
     splits = (int)((M + chunk - 1) / chunk);
@@ -965,11 +966,17 @@ int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, 
             return v ? atoi(v) : 0;
         }();
         w.diag = diag;
-        hipLaunchKernelGGL(k_wgrad_glds, dim3((unsigned)splits), dim3(512), kGNB * kGChunkB, st, w);
+        // 32-row chunks dealt round robin over the workgroups: the caller's split count (at most
+        // one chunk each), not the range-normalised one above -- the same rule as launch_wgrad_l1,
+        // so the H1-copy and recompute paths give each slab the same rows (bit-identical dW2)
+        const int gs = (int)(requested < M / kGK ? requested : M / kGK);
+        DXRL_REQUIRE(gs == 1 || partial, "wgrad: split-K needs a partial slab");
+        w.partial = gs > 1 ? partial : nullptr;
+        hipLaunchKernelGGL(k_wgrad_glds, dim3((unsigned)gs), dim3(512), kGNB * kGChunkB, st, w);
         if (int rc = launch_check("k_wgrad_glds")) return rc;
-        if (splits > 1) {
+        if (gs > 1) {
             const int64_t slab = (int64_t)O * I;
-            return launch_slab_reduce(partial, slab, splits, partial + (int64_t)splits * slab, out, 0, st, I, ldo);
+            return launch_slab_reduce(partial, slab, gs, partial + (int64_t)gs * slab, out, 0, st, I, ldo);
         }
         return DXRL_OK;
     }

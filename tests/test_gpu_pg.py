@@ -165,13 +165,15 @@ def test_fused_learner_matches_gemm_chain(pkg, n, T, h1_recompute):
         assert math.isclose(lf[k], lu[k], rel_tol=1e-4, abs_tol=1e-7), (k, lf[k], lu[k])
 
 
-def test_h1_recompute_is_bit_exact(pkg):
+@pytest.mark.parametrize("n,T", [(256, 32), (773, 32), (5, 32), (1, 96)])
+def test_h1_recompute_is_bit_exact(pkg, n, T):
     """dW2 from H1 recomputed on chip (k_wgrad_l1) == dW2 from the H1 HBM copy, bit for bit:
     the recompute repeats the learner forward's L1 exactly and both contractions sum in the
-    same order."""
+    same order.  Sizes: 32 chunks per workgroup; 32-33 (ragged over 24 splits); 5 and 3 chunks
+    in one workgroup (shorter than the chunk ring's look-ahead)."""
     grads = []
     for rec in (True, False):
-        _, tr = make(pkg, 256, 32, fused=True, h1_recompute=rec)
+        _, tr = make(pkg, n, T, fused=True, h1_recompute=rec)
         tr.rollout()
         for name in [x for x in tr.phases() if x not in ("rollout", "optimizer_step")]:
             getattr(tr, name)()

@@ -99,9 +99,11 @@ def test_rollout_policy_matches_training_forward(pkg, fused):
     assert s["clip_frac"] == 0.0 and abs(s["approx_kl"]) < 1e-9
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_iteration_matches_torch_reference(pkg, fused):
-    n, T = 256, 32
+@pytest.mark.parametrize("n,T,fused", [(256, 32, True), (256, 32, False), (773, 32, True), (5, 32, True),
+                                       (100, 40, False)])
+def test_iteration_matches_torch_reference(pkg, n, T, fused):
+    """One learner pass vs the torch fp32 restatement; 773 x 32: ragged last 128-sample tile and
+    24 dW2 slabs of 32-33 chunks; 5 x 32: one partial tile, one slab."""
     env, tr = make(pkg, n, T, fused=fused)
     _learner_pass(tr)
     cfg = dict(gamma=tr.cfg.gamma, lam=tr.cfg.lam, clip_eps=tr.cfg.clip_eps, vf_coef=tr.cfg.vf_coef,

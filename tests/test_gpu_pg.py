@@ -357,6 +357,36 @@ def test_minibatch_gradients_sum_to_full_batch(pkg):
         assert abs(0.5 * (losses[0][k] + losses[1][k]) - losses[2][k]) <= 1e-5 * max(1.0, abs(losses[2][k])), k
 
 
+def test_unequal_minibatch_gradients_weight_to_full_batch(pkg):
+    """Unequal time-contiguous slices M/4, M/2, M/4 at a ragged size (772 x 32: the slices start
+    inside a 128-sample tile, end on a partial one, and deal 32-33 dW2 chunks per slab):
+    sum_k rows_k / M x grad_k == the full-batch gradient.  Power-of-two row ratios keep the
+    per-sample loss scale's bf16 roundings identical across passes, so the tolerance is f32
+    summation order only (with a 1/9600-vs-1/24736 split the scaled bf16 head gradients round
+    differently and W1a moves by ~4e-3)."""
+    env, tr = make(pkg, 772, 32)
+    for name in ("rollout", "critic_values", "advantages"):
+        getattr(tr, name)()
+    M = tr.M
+    q = M // 4
+    assert q % 32 == 0 and q % 128
+    slices = ((0, q), (q, 2 * q), (3 * q, q), (0, M))
+    got = []
+    for mb in slices:
+        tr._mb = mb
+        tr.actor_train()
+        tr.critic_train()
+        torch.cuda.synchronize()
+        got.append(tr.grads.clone())
+    w = [rows / M for _, rows in slices[:3]]
+    for name in ("W1a", "W2a", "W3a", "W1c", "W2c", "W3c"):  # biases ride in each block's extra column
+        a = sum(wk * tr.block(name, g) for wk, g in zip(w, got))
+        b = tr.block(name, got[3])
+        assert ((a - b).norm() / b.norm()).item() < 1e-5, name
+    ls = slice(pkg.trainer.OFF["logstd"], pkg.trainer.OFF["logstd"] + 15)
+    torch.testing.assert_close(sum(wk * g[ls] for wk, g in zip(w, got)), got[3][ls], rtol=1e-5, atol=1e-7)
+
+
 def test_ppo_epochs_engage_the_clip(pkg):
     """epochs x minibatches > 1: after the first Adam step the ratio leaves 1, so the later
     minibatches see a nonzero KL and (with a large learning rate) clipped samples."""

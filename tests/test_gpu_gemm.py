@@ -97,7 +97,8 @@ def wgrad(N, Y, O, X, I, splits=1):
 @pytest.mark.parametrize("M,O,ldy,I,ldx,splits", [(64, 128, 128, 128, 128, 1), (1000, 256, 256, 288, 288, 1),
                                                   (4096, 32, 32, 288, 288, 7), (3232, 256, 256, 64, 64, 5),
                                                   (50016, 256, 256, 288, 288, 33), (1000, 200, 256, 264, 288, 4),
-                                                  (819200, 256, 256, 256, 288, 256), (5000, 256, 256, 288, 288, 4)])
+                                                  (819200, 256, 256, 256, 288, 256), (5000, 256, 256, 288, 288, 4),
+                                                  (96, 256, 256, 256, 256, 7), (24736, 256, 256, 256, 256, 24)])
 def test_wgrad_transposed_lds_reads(N, M, O, ldy, I, ldx, splits):
     """out[o][i] = sum_m Y[m][o] X[m][i] from row-major operands (ds_read_b64_tr_b16 path)."""
     g = torch.Generator(device="cuda").manual_seed(M + O + I)

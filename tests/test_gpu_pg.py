@@ -387,10 +387,12 @@ def test_unequal_minibatch_gradients_weight_to_full_batch(pkg):
     torch.testing.assert_close(sum(wk * g[ls] for wk, g in zip(w, got)), got[3][ls], rtol=1e-5, atol=1e-7)
 
 
-def test_ppo_epochs_engage_the_clip(pkg):
+@pytest.mark.parametrize("n", [256, 772])
+def test_ppo_epochs_engage_the_clip(pkg, n):
     """epochs x minibatches > 1: after the first Adam step the ratio leaves 1, so the later
-    minibatches see a nonzero KL and (with a large learning rate) clipped samples."""
-    env, tr = make(pkg, 256, 32, epochs=3, minibatches=4, lr=3e-3)
+    minibatches see a nonzero KL and (with a large learning rate) clipped samples.  772 x 32:
+    minibatch slices that start inside a 128-sample tile."""
+    env, tr = make(pkg, n, 32, epochs=3, minibatches=4, lr=3e-3)
     assert "ppo_updates" in tr.phases()
     p0 = tr.params.clone()
     tr.iteration()

@@ -84,8 +84,12 @@ def parse():
     p.add_argument("--sched-restart", action="store_true",
                    help="C3: restart the CurriculumScheduler from its initial config at the start of every "
                         "iteration (CurriculumScheduler.reset()), so every timed iteration replays progressions")
-    p.add_argument("--no-overlap", action="store_true",
-                   help="collectives on the compute stream (TrainerConfig.overlap_comm=False)")
+    p.add_argument("--overlap", action="store_true",
+                   help="exchanges on a side stream beside the train passes (TrainerConfig.overlap_comm=True; "
+                        "default: serialised on the compute stream, DESIGN.md §7)")
+    p.add_argument("--reserve-cus", type=int, default=0,
+                   help="CUs kept free of the persistent learner kernels for the side-stream collectives "
+                        "(TrainerConfig.reserve_cus)")
     p.add_argument("--dist", action="store_true",
                    help="create the RCCL process group even at --gpus 1 (before any GPU work) and run the "
                         "multi-rank code path: the trainer's collectives, barrier and max-over-ranks timing")
@@ -177,8 +181,10 @@ def pg_bench(args, world, rank, dev):
         import torch.distributed as dist
         pg = dist.group.WORLD
     kw = {"success_rule": args.success_rule} if args.success_rule else {}
-    if args.no_overlap:
-        kw["overlap_comm"] = False
+    if args.overlap:
+        kw["overlap_comm"] = True
+    if args.reserve_cus:
+        kw["reserve_cus"] = args.reserve_cus
     env, tr = build_pg_workload(args.config, dev, rank=rank, world=world, process_group=pg, envs=args.envs,
                                 horizon=args.horizon, curriculum=args.curriculum, epochs=args.epochs,
                                 minibatches=args.minibatches, **kw)
@@ -461,7 +467,8 @@ def main():
         "config": {"workload": workload, "learner": args.learner, "envs_per_gpu": args.envs,
                    "global_envs": args.envs * world, "horizon": args.horizon, "parallelism": par,
                    "world_size": world,
-                   "backend": "nccl (RCCL over xGMI)" if world > 1 or args.dist else None},
+                   "backend": "nccl (RCCL over xGMI)" if world > 1 or args.dist else None,
+                   "overlap_comm": bool(args.overlap), "reserve_cus": args.reserve_cus},
     }
     out.update(extra)
     # peak torch-allocated device memory of the bench itself (trainer buffers, tapes), read

@@ -7,13 +7,14 @@ correctly rounded f32 division/sqrt.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
-SOURCES = ["dxrl_env.hip", "dxrl_rollout.hip", "dxrl_gemm.hip", "dxrl_pg.hip", "dxrl_pg_fused.hip", "dxrl_eval.hip", "dxrl_sched.hip"]
-HEADERS = ["dxrl_device.h", "dxrl_internal.h", "dxrl_mfma.h", "dxrl_gemm.h", "dxrl_pg.h"]
+SOURCES = ["dxrl_env.hip", "dxrl_rollout.hip", "dxrl_gemm.hip", "dxrl_pg.hip", "dxrl_pg_fused.hip", "dxrl_pg_rollout8.hip", "dxrl_eval.hip", "dxrl_sched.hip"]
+HEADERS = ["dxrl_device.h", "dxrl_internal.h", "dxrl_mfma.h", "dxrl_gemm.h", "dxrl_pg.h", "dxrl_pg_rollout.h"]
 OUT = os.path.join(PKG_DIR, "libdxrl.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -27,6 +28,7 @@ def _inputs():
     root = os.path.dirname(PKG_DIR)
     files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     files.append(os.path.join(root, "include", "dxrl.h"))
+    files.append(os.path.abspath(__file__))  # a flag change here must rebuild the library
     return files
 
 
@@ -74,12 +76,20 @@ def build_native(force: bool = False, verbose: bool = False, asan: bool = False)
     def obj(src):
         o = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
         s = os.path.join(CSRC, src)
-        if force or not os.path.exists(o) or os.path.getmtime(o) < max(hdr_t, os.path.getmtime(s)):
-            cmd = [HIPCC, *compile_flags, *extra, "-c", "-o", o + ".tmp", s]
+        cmd = [HIPCC, *compile_flags, *extra, "-c", "-o", o + ".tmp", s]
+        # the compile command's hash sits next to the object: a change of FLAGS, HIPCC or the
+        # sanitizer options rebuilds it even when no source is newer
+        stamp = o + ".cmd"
+        digest = hashlib.sha256("\0".join(cmd).encode()).hexdigest()
+        old = open(stamp).read().strip() if os.path.exists(stamp) else ""
+        if (force or old != digest or not os.path.exists(o)
+                or os.path.getmtime(o) < max(hdr_t, os.path.getmtime(s))):
             if verbose:
                 print(" ".join(cmd), flush=True)
             subprocess.run(cmd, check=True, cwd=CSRC)
             os.replace(o + ".tmp", o)
+            with open(stamp, "w") as f:
+                f.write(digest + "\n")
         return o
 
     with ThreadPoolExecutor(_jobs()) as ex:

@@ -12,6 +12,7 @@
 // No inter-workgroup communication: envs and weights are independent/read-only.
 #include "dxrl_gemm.h"
 #include "dxrl_pg.h"
+#include "dxrl_pg_rollout.h"
 
 #include <stdio.h>
 
@@ -21,8 +22,6 @@ using namespace dxrl;
 using namespace dxrl::pg;
 
 namespace dxrl {
-
-constexpr float kLog2Pi = 1.8378770664093453f;
 
 // log N(a | mu, sigma) summed over the action dims
 __device__ __forceinline__ float gauss_logp(const float* a, const float* mu, const float* logstd) {
@@ -51,41 +50,6 @@ __device__ __forceinline__ void philox_normals(float* out, uint32_t k0, uint32_t
     }
 }
 
-struct PgRolloutArgs {
-    EnvSoA s;
-    Weights w;
-    int max_episode_steps, max_steps, horizon;
-    const bf16* wbf;
-    const float* params;
-    uint64_t env_seed, policy_seed;
-    int64_t gid0;
-    uint64_t iteration;
-    float obs_noise, dyn_noise;
-    bf16* obs_rm;   // [(T+1) N][kIn]
-    bf16* obs_fm;   // [kIn][T N]
-    float* act;     // [T N][kActPad]
-    float* logp;    // [T N]
-    float* rew;     // [T N]
-    uint8_t* done;  // [T N]
-    double* ep_ret; // [N] open-episode return (persists across calls)
-    int32_t* ep_count;
-    double* ep_sum_ret;
-    int32_t* ep_sum_len;
-    int32_t* ep_succ;
-    int diag;       // timing ablations: bit0 skip actor MLP, bit1 skip env step
-    int success_terminated;
-    int record_cap;
-    double* rec_return;
-    int32_t* rec_length;
-    uint8_t* rec_success;
-    int32_t* rec_end_step;
-    uint16_t* ep_code;   // [T N] scheduler feed: 0, or (episode length << 1) | success (nullable)
-    float* applied_act;  // [T N][kActPad] the action the env integrated (nullable; parity checks)
-    float* dyn_noise_tape;  // [T N][kActPad] f32(sigma) * z as added to the action (nullable; ws kernel)
-    float* obs_noise_tape;  // [(T+1) N][kObsNoiseLd] f32(sigma) * z per observation element (nullable)
-    unsigned long long* stamps;  // diag & 32 (k_pg_rollout_ls): cycles per step segment
-};
-constexpr int kObsNoiseLd = 48;
 
 constexpr int kTile = 64;           // envs per workgroup
 constexpr int kXs = kIn + 8;        // LDS row strides (bf16) -- conflict-free b128 fragment reads
@@ -247,7 +211,6 @@ __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfr
 // chunks XOR-swizzled by the row (chunk c of row r at chunk c ^ r, r < 16; swz16): the fragment
 // reads (ds_read_b128, lane groups of 16) are then conflict-free and the 8-byte epilogue stores
 // stay 2-way, where the padded 264-element pitch made every fragment read 2-way.
-__device__ __forceinline__ int swz16(int r, int col) { return ((((col >> 3) ^ r) << 3) | (col & 7)); }
 template <int KS, int NT, bool kSwzA = false, bool kSwzOut = false, typename WF>
 __device__ __forceinline__ void wave_layer16(const bf16* A, int lda, const WF& wfrag, int n0, bf16* out, int ldo,
                                              int lane, const float* bias_v = nullptr) {
@@ -891,15 +854,6 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
 // Exchanges inside an env's 16 lanes are DPP row broadcasts (an env is one DPP row).
 constexpr int kWsWaves = 8, kWsThreads = 64 * kWsWaves;
 
-// Workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding
-// global store (s_waitcnt vmcnt(0)) before s_barrier, which puts the tape stores' write
-// latency on each step's critical path.  Nothing here is handed between waves through global
-// memory, so only LDS is fenced.
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 
 // One env lane's draws, computed by its aux twin (structure of arrays over the 256 env lanes):
 // the action / dynamics noise normals and the reset uniforms (at the env's exact reset counter)
@@ -2142,9 +2096,24 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
         stamps_n = n;
     }
     p.stamps = stamps;
+    static const int cus = [] {
+        int dev = 0, c = 0;
+        (void)hipGetDevice(&dev);
+        return hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0 ? c : 256;
+    }();
+    // >= 32 envs per CU: the 32-env kernel runs them in one round (the 16-env kernel would need
+    // two); diag 1024 / 2048 force the 32-env / 16-env kernel (A/B, bit-identity tests)
+    const bool e8 = !(a->diag_flags & (32 | 64 | 2048)) && ((a->diag_flags & 1024) || n >= (int64_t)kE8Envs * cus);
+    if (e8) {
+        const bool noise = a->obs_noise_std > 0.0 || a->dyn_noise_std > 0.0 || a->dyn_noise_tape || a->obs_noise_tape;
+        const bool diag = (a->diag_flags & ~(1024 | 2048)) != 0 || a->applied_act || a->dyn_noise_tape ||
+                          a->obs_noise_tape;
+        return launch_pg_rollout_e8(p, n, noise, diag, as_stream(stream));
+    }
     if (!(a->diag_flags & (32 | 64))) {  // default: the warp-specialised kernel
         const bool noise = a->obs_noise_std > 0.0 || a->dyn_noise_std > 0.0 || a->dyn_noise_tape || a->obs_noise_tape;
-        const bool diag = a->diag_flags != 0 || a->applied_act || a->dyn_noise_tape || a->obs_noise_tape;
+        const bool diag = (a->diag_flags & ~(1024 | 2048)) != 0 || a->applied_act || a->dyn_noise_tape ||
+                          a->obs_noise_tape;
         const dim3 grid((unsigned)((n + kLsEnvs - 1) / kLsEnvs)), block(kWsThreads);
         if (noise && diag) hipLaunchKernelGGL((k_pg_rollout_ws<true, true>), grid, block, 0, as_stream(stream), p);
         else if (noise) hipLaunchKernelGGL((k_pg_rollout_ws<true, false>), grid, block, 0, as_stream(stream), p);

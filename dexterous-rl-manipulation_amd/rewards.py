@@ -51,9 +51,17 @@ def _device_compute(kind: int, weights, joint_positions, finger_tips, object_pos
         if not (jp.shape[0] == tips.shape[0] == op.shape[0] == B):
             raise ValueError("joint_positions, finger_tips, object_position and contacts disagree on the batch size")
         prev, has = state
-        if prev is None or prev.shape[0] != B:
+        if prev is None:
             prev = torch.zeros(B, num_fingers, dtype=torch.float32, device=dev)
             has = torch.zeros(B, dtype=torch.uint8, device=dev)
+        elif prev.shape[0] != B:
+            raise ValueError(f"batch size changed from {prev.shape[0]} to {B} while prev_contacts is set: call "
+                             "reset() first (the stability term compares each row with its own previous contacts)")
+        else:
+            # the kernel updates the previous contacts in place; the tensor handed out as
+            # prev_contacts after the last call (or assigned by the caller) must stay as it was,
+            # as the reference's contacts.copy() leaves it (reward_shaping.py:174,185)
+            prev, has = prev.clone(), has.clone()
         w = (C.c_double * 4)(*weights)
     out = torch.empty(B, 5, dtype=torch.float64, device=dev)
     N.call("dxrl_reward_compute", dev.index, kind, w, B, num_fingers, joints_per_finger, N.ptr(jp), N.ptr(tips),
@@ -123,7 +131,7 @@ class RewardShaping:
         from . import _native as N
         dev = N.require_gpu(self.device)
         p = torch.as_tensor(np.asarray(prev) if not isinstance(prev, torch.Tensor) else prev)
-        p = p.to(device=dev, dtype=torch.float32).reshape(-1, F).contiguous()
+        p = p.to(device=dev, dtype=torch.float32).reshape(-1, F).clone()  # never the caller's own tensor
         return p, torch.ones(p.shape[0], dtype=torch.uint8, device=dev)
 
 

@@ -88,6 +88,11 @@ class TrainerConfig:
     # at world 1 over RCCL the overlapped form costs 85 us per iteration, the serialised one 31 us
     # (profiles/r04/ab_dist_overlap.log).  Both give bit-identical results.
     overlap_comm: bool = False
+    # CUs left free of the persistent learner kernels (k_pg_fused, k_wgrad_l1): their grids become
+    # CUs - reserve_cus, so a collective on the comm stream has CUs of its own to run on beside them
+    # (overlap_comm); 0 = every CU.  Changes the learner's per-workgroup partial-sum order (so the
+    # gradients' last bits), not the sums themselves; overlapped == serialised holds at any value.
+    reserve_cus: int = 0
 
 
 def minibatch_bounds(M: int, B: int, round_samples: int):
@@ -151,6 +156,8 @@ class PGTrainer:
         if self.collective and cfg.overlap_comm and env.device.type == "cuda":
             self._comm = torch.cuda.Stream(device=env.device)
         self._stats_pending = self._grads_pending = False
+        self._stats_event = torch.cuda.Event() if self._comm is not None else None
+        self._update_follows = True  # iteration(update=False) clears it for its train passes
         self.global_M = global_count(self.M, self.world, self.pg)  # samples of all ranks per iteration
         if self.global_M != self.M * self.world:
             raise ValueError(f"every rank needs the same num_envs * horizon ({self.M} here, {self.global_M} over "
@@ -212,13 +219,21 @@ class PGTrainer:
         nb = max(512, N.gae_partial_doubles(n, T))
         self.partial = torch.zeros(nb, dtype=torch.float64, device=d)
         self.dH2 = z(M, H, dt=bf)
-        self.splits = max(1, min(cfg.splitk_target_blocks // 3, M // 1024))  # dW2: one workgroup per CU
+        cus = int(torch.cuda.get_device_properties(d).multi_processor_count)
+        if not 0 <= int(cfg.reserve_cus) < cus:
+            raise ValueError(f"reserve_cus must be in [0, {cus})")
+        self.learner_cus = cus - int(cfg.reserve_cus)  # CUs the persistent learner grids use
+        # dW2: one workgroup per (learner) CU
+        self.splits = max(1, min(cfg.splitk_target_blocks // 3, M // 1024))
+        if self.learner_cus < cus:
+            self.splits = min(self.splits, self.learner_cus)
         self.kpartial = z(self.splits + 16, H, HX)  # + two-level reduction scratch
         self.gnorm2 = torch.zeros(1, dtype=torch.float64, device=d)
         tr_, pf_ = C.c_int32(), C.c_int64()
         N.call("dxrl_pg_fused_sizes", C.byref(tr_), C.byref(pf_))
         # up to two learner workgroups per CU (64-sample tiles); the library clamps to its geometry
-        self.fused_grid = 2 * int(torch.cuda.get_device_properties(d).multi_processor_count)
+        # (one 128-sample workgroup per CU), so a reservation passes the CU count itself
+        self.fused_grid = 2 * cus if self.learner_cus == cus else self.learner_cus
         self.fused_partial = z(self.fused_grid + 17, pf_.value)  # + reduction scratch and sum
         self.fused_loss = torch.zeros(self.fused_grid, 4, dtype=torch.float64, device=d)
         self.pack()
@@ -329,7 +344,9 @@ class PGTrainer:
         start, rows = self._mb
         self._loss_rows = rows
         if self._stats_pending:  # the actor's head normalises the advantages with the global moments
-            torch.cuda.current_stream(self.dev).wait_stream(self._comm)
+            # only the moments: the critic half's all-reduce queued behind them on the comm stream
+            # runs beside this pass
+            torch.cuda.current_stream(self.dev).wait_event(self._stats_event)
             self._stats_pending = False
         N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(0, True, rows, start)), self._s())
 
@@ -337,7 +354,10 @@ class PGTrainer:
         start, rows = self._mb
         self._loss_rows = rows
         N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(1, True, rows, start)), self._s())
-        if self._comm is not None:  # the critic half's SUM all-reduce runs beside the actor's pass
+        # the critic half's SUM all-reduce runs beside the actor's pass -- only when an optimiser
+        # step follows (iteration(update=False) issues no gradient collective, as the serialised
+        # form does not, and leaves nothing in flight that the next pass's gradients would race)
+        if self._comm is not None and self._update_follows:
             with self._on_comm():
                 self._allreduce(self.grads[OFF["W1c"]:])
             self._grads_pending = True
@@ -358,7 +378,7 @@ class PGTrainer:
         self._mb = (0, self.M)
 
     def minibatch_bounds(self):
-        return minibatch_bounds(self.M, self.cfg.minibatches, 128 * (self.fused_grid // 2))
+        return minibatch_bounds(self.M, self.cfg.minibatches, 128 * self.learner_cus)
 
     def phases(self):
         """The iteration's launch groups in order (bench.py times each)."""
@@ -387,6 +407,8 @@ class PGTrainer:
                 gather_adv_moments_(self.moments_all, self.stats, self.world, self.pg)
                 N.call("dxrl_pg_adv_combine", self.dev.index, N.ptr(self.moments_all), self.world,
                        N.ptr(self.stats), self._s())
+                if self._comm is not None:
+                    self._stats_event.record(self._comm)
             self._stats_pending = self._comm is not None
 
     def _on_comm(self):
@@ -607,13 +629,19 @@ class PGTrainer:
     def iteration(self, update: bool = True):
         from . import profiling
         marks = profiling.enabled()
-        for name in self.phases():
-            with profiling.range_(f"pg.{name}") if marks else _null():
-                if name == "ppo_updates" and not update:
-                    self.critic_train()
-                    self.actor_train()
-                elif name != "optimizer_step" or update:
-                    getattr(self, name)()
+        self._update_follows = update
+        try:
+            for name in self.phases():
+                with profiling.range_(f"pg.{name}") if marks else _null():
+                    if name == "ppo_updates" and not update:
+                        self.critic_train()
+                        self.actor_train()
+                    elif name != "optimizer_step" or update:
+                        getattr(self, name)()
+        finally:
+            self._update_follows = True
+        if not update:
+            self._join_comm()  # nothing of this iteration's exchanges stays in flight
         self.iteration_index += 1
 
     # ------------------------------------------------------------------ stats

@@ -1,4 +1,4 @@
-"""CPU, world_size 2 and 3 over gloo: the sharded learner decomposition equals the
+"""CPU, world_size 2, 3 and 8 over gloo: the sharded learner decomposition equals the
 single-process learner on the concatenated batch.
 
 Each rank takes its shard of the envs (distributed.shard_range), runs the same
@@ -45,7 +45,7 @@ def _worker(rank, world, port, out):
     import dexterous_rl_manipulation_amd  # noqa: F401
     from dexterous_rl_manipulation_amd import distributed as D
     topo = D.init_from_env(backend="gloo")
-    n, T = 9, 6  # 9 envs: ragged shards for world 2 (4 + 5) and even ones for world 3
+    n, T = 9, 6  # 9 envs: ragged shards for world 2 (4 + 5) and 8 (2 + 7 x 1), even ones for world 3
     params, obs, act, logp_old, rew, done = make_case(n, T, seed=3)
     full, full_info = R.loss_and_grads(params, obs, act, logp_old, rew, done, n, T, CFG, bf16=False)
     lo, hi = D.shard_range(n, world, rank)
@@ -99,7 +99,7 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_exchange_equals_concatenated_batch(world):
     ctx = mp.get_context("spawn")
     out = ctx.Manager().dict()

@@ -1,4 +1,4 @@
-"""GPU, multi-rank: PGTrainer sharded over two ranks (two processes on cuda:0, gloo
+"""GPU, multi-rank: PGTrainer sharded over two and four ranks (processes on cuda:0, gloo
 process group -- RCCL needs one GPU per rank, which a one-GPU test box does not
 have) equals the world-1 trainer on the concatenated batch ("the
 8-rank loss/params must equal 1-rank on the concatenated batch within fp32
@@ -40,30 +40,36 @@ def _launch(tmp, world, n, iters, config, overlap=True):
     return [torch.load(o, weights_only=False) for o in outs]
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("config", ["variable", "default"])
-def test_two_ranks_equal_one_rank_on_concatenated_batch(tmp_path, config):
-    n, iters = 256, 3
-    one = _launch(str(tmp_path), 1, 2 * n, iters, config)[0]
-    two = _launch(str(tmp_path), 2, n, iters, config)
+def test_ranks_equal_one_rank_on_concatenated_batch(tmp_path, config, world):
+    """world ranks of n envs == one rank of world x n envs (512 global envs either way; world 4
+    drives the trainer's rank-order logic -- the moment merge, the C3 pack walk in (end step,
+    global env id) order and the candidate-step all-reduce -- past two ranks)."""
+    n, iters = 512 // world, 3
+    one = _launch(str(tmp_path), 1, world * n, iters, config)[0]
+    many = _launch(str(tmp_path), world, n, iters, config)
     # the first iteration's tapes: rank r holds env columns [r n, (r+1) n) of the world-1 run
-    for r, res in enumerate(two):
+    for r, res in enumerate(many):
         assert torch.equal(res["rew0"], one["rew0"][:, r * n:(r + 1) * n])
         assert torch.equal(res["done0"], one["done0"][:, r * n:(r + 1) * n])
     # every rank ends with the same parameters (identical Adam inputs after the all-reduce)
-    assert torch.equal(two[0]["params"], two[1]["params"])
+    for r in range(1, world):
+        assert torch.equal(many[0]["params"], many[r]["params"]), r
+        assert torch.equal(many[0]["stats0"], many[r]["stats0"]), r
     # global advantage moments and normalisation == world 1 (f64, summation order only)
     for k in (0, 1, 2, 4):
-        a, b = two[0]["stats0"][k].item(), one["stats0"][k].item()
+        a, b = many[0]["stats0"][k].item(), one["stats0"][k].item()
         assert abs(a - b) <= 1e-9 * max(1.0, abs(b)), (k, a, b)
     # the first iteration's all-reduced gradient == the world-1 gradient (f32 summation order)
-    g2, g1 = two[0]["grads0"], one["grads0"]
-    rel = (g2 - g1).norm() / g1.norm()
+    gw, g1 = many[0]["grads0"], one["grads0"]
+    rel = (gw - g1).norm() / g1.norm()
     assert rel < 1e-4, rel.item()
     # after `iters` Adam steps the parameters still agree to f32 reduction-order tolerance
-    p2, p1 = two[0]["params"], one["params"]
-    assert (p2 - p1).abs().max().item() < 1e-4 * max(1.0, p1.abs().max().item())
+    pw, p1 = many[0]["params"], one["params"]
+    assert (pw - p1).abs().max().item() < 1e-4 * max(1.0, p1.abs().max().item())
     if config == "default":
-        assert two[0]["sched"] == two[1]["sched"] == one["sched"]
+        assert all(res["sched"] == one["sched"] for res in many)
 
 
 @pytest.mark.parametrize("config", ["variable", "default"])

@@ -67,7 +67,8 @@ def _oracle_cur(c):
 
 
 def _lanes(n, k=32, seed=0):
-    probe = [0, 1, 15, 16, 17, 31, 32, 255, 256, n // 2 - 1, n // 2, n - 17, n - 16, n - 1]
+    probe = [0, 1, 7, 8, 15, 16, 17, 31, 32, 63, 64, 255, 256, n // 2 - 1, n // 2, n - 33, n - 32, n - 17, n - 16,
+             n - 1]
     rng = np.random.default_rng(seed)
     rest = rng.choice(np.setdiff1d(np.arange(n), probe), k - len(probe) + 4, replace=False)
     return sorted(set(probe) | set(int(x) for x in rest))
@@ -246,6 +247,37 @@ def test_benched_rollout_equals_parity_instantiation(pkg, name):
     for k in a:
         assert a[k].view(torch.uint8).equal(b[k].view(torch.uint8)), (name, k)
     assert int(a["ep_count"].sum()) > 0
+
+
+@pytest.mark.parametrize("name", ["hard_heldout", "variable_noise"])
+def test_32_env_kernel_equals_16_env_kernel_at_full_size(pkg, name):
+    """At C4's 8192 envs (32 per CU) the rollout runs k_pg_rollout_e8 (8 lanes per env, 32 envs
+    per workgroup, one round); the 16-env k_pg_rollout_ws (diag 2048) must give the same tapes,
+    per-env sums, records and env state bit for bit, over two iterations (mid-episode state and
+    moved Philox counters in the second).  variable_noise at 8192 envs runs the e8 kernel's
+    fused observation / dynamics noise."""
+    dev = torch.device("cuda", 0)
+    outs = []
+    for diag in (0, 2048):
+        env, tr = pkg.workloads.build_pg_workload(name, dev, envs=8192, record_cap=8)
+        if tr.ep_code is None:
+            tr.ep_code = torch.zeros(tr.M, dtype=torch.int16, device=dev)
+        tr.diag_flags = diag
+        for _ in range(2):
+            tr.rollout()
+            tr.iteration_index += 1
+        torch.cuda.synchronize()
+        outs.append({k: getattr(tr, k).clone() for k in (
+            "obs_rm", "act", "logp", "rew", "done", "ep_count", "ep_sum_ret", "ep_sum_len", "ep_succ", "rec_return",
+            "rec_length", "rec_success", "rec_end", "ep_code", "ep_ret")} | {"state": env.state.clone()})
+        del env, tr
+    a, b = outs
+    for k in a:
+        assert a[k].view(torch.uint8).equal(b[k].view(torch.uint8)), (name, k)
+    assert int(a["ep_count"].sum()) > 0
+
+
+def test_normalisation_large_mean(pkg):
     """The normalisation moments with |mean| / std > 1e3 (every step its own episode,
     A = r - V, rewards shifted by 1e4): a one-pass sum(a^2) - mean sum(a) lost 2.8e-6 of
     the std here; the merged (count, mean, M2) moments (k_gae / k_gae_sums /

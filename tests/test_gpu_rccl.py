@@ -7,7 +7,9 @@ global_count SUM and the f64 MAX.  Each must return its input; and a PGTrainer d
 through that group (3 full iterations, curriculum-scheduler and fused-noise configs) must
 give the group-less trainer's gradients, statistics, episode codes and parameters bit for
 bit -- with its exchanges on the side stream overlapping the train passes (overlap_comm=True) and
-serialised on the compute stream (overlap_comm=False, the default).  Multi-rank semantics are covered by tests/test_dist_gloo.py (CPU) and
+serialised on the compute stream (overlap_comm=False, the default), with an iteration(update=False)
+between updates (the overlapped form then issues no gradient collective and leaves none in
+flight), and with CUs reserved for the collectives (reserve_cus).  Multi-rank semantics are covered by tests/test_dist_gloo.py (CPU) and
 tests/test_gpu_dist.py (two ranks on one GPU over gloo)."""
 import os
 import socket
@@ -48,3 +50,13 @@ def test_rccl_world1_collectives_and_trainer(tmp_path):
             assert torch.equal(a["params"], other["params"]), config
             if config == "default":
                 assert a["sched"] == other["sched"]
+        for suffix in ("_noupdate", "_reserve"):
+            a, b = res[config + suffix]
+            assert a["overlapped"] and a["collective"]
+            for k in ("grads", "stats", "codes"):
+                assert len(a[k]) == len(b[k])
+                for x, y in zip(a[k], b[k]):
+                    assert torch.equal(x, y), (config, suffix, k)
+            assert torch.equal(a["params"], b["params"]), (config, suffix)
+            if config == "default":
+                assert a["sched"] == b["sched"]

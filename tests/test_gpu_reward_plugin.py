@@ -111,3 +111,31 @@ def test_sparse_compute_counts_contacts(R):
     assert d == {"total": 1.0, "distance": 0.0, "contact": 0.0, "closure": 0.0, "stability": 0.0}
     with pytest.raises(ValueError, match="num_fingers"):
         R.SparseReward().compute(None, None, None, np.ones(4, np.float32), 4, 3)
+
+
+def test_compute_never_writes_caller_tensors_and_rejects_batch_change(R):
+    """prev_contacts handed in (a device f32 tensor) or handed out by the previous call stays as
+    it was after the next call (the reference replaces it by contacts.copy(), :174, :185); a
+    changed batch size while a state is held is an error, not a silent reset of the state."""
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(11)
+    B = 33
+    jp = rng.uniform(-1, 1, (B, 15)).astype(np.float32)
+    tips = rng.uniform(-0.3, 0.3, (B, 5, 3))
+    op = rng.uniform(-0.2, 0.3, (B, 3))
+    con = rng.choice(np.array([0.0, 1.0], np.float32), (B, 5))
+    plugin = R.RewardShaping()
+    mine = torch.as_tensor(rng.random((B, 5)).astype(np.float32), device=dev)
+    keep = mine.clone()
+    plugin.prev_contacts = mine
+    plugin.compute(jp, tips, op, con, 5, 3)
+    assert torch.equal(mine, keep)
+    handed = plugin.prev_contacts
+    snap = handed.clone()
+    plugin.compute(jp, tips, op, 1.0 - con, 5, 3)
+    assert torch.equal(handed, snap)
+    assert torch.equal(plugin.prev_contacts.cpu(), torch.as_tensor(1.0 - con))
+    with pytest.raises(ValueError, match="batch size changed"):
+        plugin.compute(jp[:7], tips[:7], op[:7], con[:7], 5, 3)
+    plugin.reset()
+    plugin.compute(jp[:7], tips[:7], op[:7], con[:7], 5, 3)

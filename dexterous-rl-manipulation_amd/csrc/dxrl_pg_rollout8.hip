@@ -17,12 +17,14 @@
 // What the 8-lane layout changes besides the envs per workgroup:
 //   * a finger's three joints are lane-local: the finger sum, the closure term's negative-joint sum
 //     and the contact test need no cross-lane shifts; the contact mask is the ballot itself;
-//   * the tip-object squared distances go to the aux twin, which forms dmin = sqrt(min) in the
-//     reward settle (the env lanes' chain loses the five f64 broadcasts and the root);
 //   * the drawing lanes finish the reset values (joint positions, sampler values) from the
 //     uniforms, so the env lanes' reset path is LDS reads;
-//   * each aux lane computes two Philox blocks per step (480 per workgroup: 128 action-noise, 352
-//     reset), issued together so their dependent round chains interleave.
+//   * the step's 480 Philox blocks (128 action-noise, 352 reset) are drawn by all 8 waves, one
+//     per lane, in the head phase;
+//   * the env lanes form dmin (the root of the least squared tip distance) for the aux twin's
+//     reward settle, as k_pg_rollout_ws does, and the 15 log-density terms of the action and the
+//     act tape; the aux twin sums the terms in action order one step later (beside the reward
+//     settle), so log pi costs no cross-lane broadcast chain.
 #include "dxrl_pg_rollout.h"
 
 #include <stdio.h>
@@ -36,6 +38,7 @@ namespace dxrl {
 namespace {
 
 constexpr int kE8Waves = 8, kE8Threads = 64 * kE8Waves;
+
 constexpr int kObsLd = 48;  // observation-noise row (floats): element k of env e at [e][k]
 
 // lanes 0..7 of each 16-lane DPP row read lane K of the row, lanes 8..15 read lane 8 + K:
@@ -141,8 +144,9 @@ struct __attribute__((aligned(16))) E8Draws {
 struct E8Samplers {  // per env and extra slot: lo + span u with a range, the constant (span NaN) without
     double lo[kE8Envs * 8], span[kE8Envs * 8];
 };
-struct E8Reward {        // an env's dense-reward inputs and episode end of one step
-    double x[kF];        // per finger: squared tip-object distance (dmin = sqrt of the minimum)
+struct __attribute__((aligned(16))) E8Reward {  // an env's reward / log pi inputs and episode end of one step
+    float term[16];      // log-density terms of the policy's action, action order (15 used)
+    double dmin;         // np.min of the fingers' tip-object distances
     uint32_t c, prev;    // contacts, previous contacts (0x100: none)
     float nacc[kF];      // per finger: sum of its negative joint positions
     int32_t len, done, te;
@@ -273,57 +277,52 @@ __global__ __launch_bounds__(kE8Threads, 1) void k_pg_rollout_e8(PgRolloutArgs p
     const bool obs_noise = kNoise && p.obs_noise > 0.0f, dyn_noise = kNoise && p.dyn_noise > 0.0f;
     const auto env_live = [&](int e) { return (int64_t)blockIdx.x * kE8Envs + e < n; };
 
-    // ---- aux, head phase: this step's Philox blocks, two per aux lane (task L and L + 256 of
-    // 480): tasks 0..127 the action noise (env q / 4, block q % 4), 128..479 the reset uniforms at
+    // ---- head phase: this step's Philox blocks, one per lane of ALL 8 waves (480 tasks on 512
+    // lanes): tasks 0..127 the action noise (env q / 4, block q % 4), 128..479 the reset uniforms at
     // each env's exact counter (env r / 11, block r % 11; slots 2 b, 2 b + 1: joint slots 0..14,
-    // extra slots 15..20).  Same blocks and arithmetic as k_pg_rollout_ws's step_draws.
+    // extra slots 15..20).  Same blocks and arithmetic as k_pg_rollout_ws's step_draws.  Waves
+    // 0, 1 (SIMDs 0, 1) draw the action noise, waves 4..7 and 2 the reset blocks, and wave 3 --
+    // which also runs the second row tile of the mu head -- the last 32.
     constexpr int kResetBlocks = (kReset + 1) / 2;
     constexpr int kActTasks = kE8Envs * 4, kTasks = kActTasks + kE8Envs * kResetBlocks;
-    static_assert(kTasks <= 512 && kActTasks <= 256, "two draw tasks per aux lane");
+    static_assert(kTasks <= kE8Threads && kActTasks == 128, "one draw task per lane");
     const auto step_draws = [&](uint64_t ctr, int64_t t_) {
-        // the task indices re-derived from a volatile lane id each step (not hoisted into
-        // long-lived registers)
+        // the task index re-derived from a volatile lane id each step (not hoisted into a
+        // long-lived register)
         int l;
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-        const int L = 64 * (wave - 4) + l;
-        const int q0 = L, q1 = L + 256;
-        const bool act0 = q0 < kActTasks;  // wave-uniform: waves 4, 5
-        const int r0 = q0 - kActTasks, r1 = q1 - kActTasks;
-        const int e0 = act0 ? q0 >> 2 : r0 / kResetBlocks, b0 = act0 ? q0 & 3 : r0 % kResetBlocks;
-        const int e1 = r1 / kResetBlocks, b1 = r1 % kResetBlocks;
-        const bool ok0 = env_live(e0), ok1 = q1 < kTasks && env_live(e1);
-        const uint64_t c0 = act0 ? ctr : RW[(t_ - 1) & 1][e0].rctr;
-        const uint64_t c1 = ok1 ? RW[(t_ - 1) & 1][e1].rctr : 0;
-        const u32x4 x0 = philox(u32x4{(uint32_t)c0, (uint32_t)(c0 >> 32), act0 ? kStreamPolicy : kStreamReset, (uint32_t)b0},
-                                KEYS[e0][act0 ? 2 : 0], KEYS[e0][act0 ? 3 : 1]);
-        const int e1c = ok1 ? e1 : 0;
-        const u32x4 x1 = philox(u32x4{(uint32_t)c1, (uint32_t)(c1 >> 32), kStreamReset, (uint32_t)b1}, KEYS[e1c][0],
-                                KEYS[e1c][1]);
-        const auto reset_out = [&](int e, int b, const u32x4& r) {
-            const double ua = u01_53(r.x, r.y), ub = u01_53(r.z, r.w);
+        // wave -> first task: 0, 64 | 384, 448 | 128, 192, 256, 320
+        const int base = wave < 2 ? 64 * wave : wave < 4 ? 384 + 64 * (wave - 2) : 128 + 64 * (wave - 4);
+        const int q = base + l;
+        if (q >= kTasks) return;
+        if (wave < 2) {  // action noise (wave-uniform branch)
+            const int e = q >> 2, b = q & 3;
+            if (!env_live(e)) return;
+            const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamPolicy, (uint32_t)b},
+                                   KEYS[e][2], KEYS[e][3]);
+            float4 nz;
+            box_muller(r.x, r.y, nz.x, nz.y);
+            box_muller(r.z, r.w, nz.z, nz.w);
+            *reinterpret_cast<float4*>(&DR.eps[16 * e + 4 * b]) = nz;
+            return;
+        }
+        const int rq = q - kActTasks, e = rq / kResetBlocks, b = rq % kResetBlocks;
+        if (!env_live(e)) return;
+        const uint64_t rc = RW[(t_ - 1) & 1][e].rctr;
+        const u32x4 r = philox(u32x4{(uint32_t)rc, (uint32_t)(rc >> 32), kStreamReset, (uint32_t)b}, KEYS[e][0],
+                               KEYS[e][1]);
+        const double ua = u01_53(r.x, r.y), ub = u01_53(r.z, r.w);
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int k = 2 * b + h;
-                const double u = h ? ub : ua;
-                if (k < kD) {
-                    DR.jp0[16 * e + k] = (float)(-0.1 + (0.1 - -0.1) * u);
-                } else if (k < kReset) {
-                    const double lo = RSMP.lo[8 * e + k - kD], span = RSMP.span[8 * e + k - kD];
-                    DR.v2[8 * e + k - kD] = span == span ? lo + span * u : lo;
-                }
-            }
-        };
-        if (ok0) {
-            if (act0) {
-                float4 nz;
-                box_muller(x0.x, x0.y, nz.x, nz.y);
-                box_muller(x0.z, x0.w, nz.z, nz.w);
-                *reinterpret_cast<float4*>(&DR.eps[16 * e0 + 4 * b0]) = nz;
-            } else {
-                reset_out(e0, b0, x0);
+        for (int h = 0; h < 2; ++h) {
+            const int k = 2 * b + h;
+            const double u = h ? ub : ua;
+            if (k < kD) {
+                DR.jp0[16 * e + k] = (float)(-0.1 + (0.1 - -0.1) * u);
+            } else if (k < kReset) {
+                const double lo = RSMP.lo[8 * e + k - kD], span = RSMP.span[8 * e + k - kD];
+                DR.v2[8 * e + k - kD] = span == span ? lo + span * u : lo;
             }
         }
-        if (ok1) reset_out(e1, b1, x1);
     };
     // ---- aux, P0: the next observation row's noise (12 blocks per env) and this step's dynamics
     // noise (4 blocks per env), two tasks per aux lane (512 per workgroup)
@@ -365,10 +364,7 @@ __global__ __launch_bounds__(kE8Threads, 1) void k_pg_rollout_e8(PgRolloutArgs p
     // ---- aux: the dense reward (RS:50-187) and the episode bookkeeping of a finished step
     const auto settle = [&](int64_t t_) {
         const E8Reward& w = RW[t_ & 1][eg];
-        double xm = w.x[0];  // np.min over the fingers' distances: the root of the least square
-#pragma unroll
-        for (int f = 1; f < kF; ++f) xm = w.x[f] < xm ? w.x[f] : xm;
-        const double dist = exp(-5.0 * sqrt(xm));
+        const double dist = exp(-5.0 * w.dmin);
         const double con = count_over_f_f64(__popc(w.c));
         float sum = 0.0f;
 #pragma unroll
@@ -448,23 +444,36 @@ __global__ __launch_bounds__(kE8Threads, 1) void k_pg_rollout_e8(PgRolloutArgs p
         }
         flags &= ~kOpIsF32;
     };
-    // ---- env lanes, P4: action, dynamics, contacts, termination, auto-reset
+    // ---- env lanes, P4: action, dynamics, contacts (and dmin for the aux twin's reward),
+    // termination, auto-reset
     const auto env_lane_step = [&](int64_t t, int64_t m) {
         bool te = false, tr = false;
-        if (env_on) {
-            if (finger) {
+        float a0[kJ], mu0[kJ];  // the policy's action and mean (log pi at the end of the step)
+        if (finger) {
 #pragma unroll
-                for (int j = 0; j < kJ; ++j) {
-                    const int k = kJ * s + j;
-                    const float mu = mlp ? MU[eg * (kOut + 1) + k] : 0.0f;
-                    float a = mu + SIG[k] * DR.eps[16 * eg + k];
-                    if (dyn_noise)  // robustness_tests.py:180-187 (the tape keeps the policy's action)
-                        a = clipf(a + p.dyn_noise * DR.dzn[16 * eg + k], -1.0f, 1.0f);
+            for (int j = 0; j < kJ; ++j) {
+                const int k = kJ * s + j;
+                mu0[j] = mlp ? MU[eg * (kOut + 1) + k] : 0.0f;
+                a0[j] = mu0[j] + SIG[k] * DR.eps[16 * eg + k];
+                p.act[m * kActPad + k] = a0[j];
+                float a = a0[j];
+                if (dyn_noise)  // robustness_tests.py:180-187 (the tape keeps the policy's action)
+                    a = clipf(a + p.dyn_noise * DR.dzn[16 * eg + k], -1.0f, 1.0f);
+                if (kDiag && p.applied_act) p.applied_act[m * kActPad + k] = a;
+                if (kDiag && p.dyn_noise_tape)
+                    p.dyn_noise_tape[m * kActPad + k] = dyn_noise ? p.dyn_noise * DR.dzn[16 * eg + k] : 0.0f;
+                if (env_on) {
                     const float ak = clipf(a, -1.0f, 1.0f);
                     jv[j] = kC09 * jv[j] + kC01 * ak;
                     jp[j] = clipf(jp[j] + jv[j] * kDt, -1.0f, 1.0f);
                 }
             }
+        } else if (s == kF) {  // the tapes' padding slot
+            p.act[m * kActPad + kAct] = 0.0f;
+            if (kDiag && p.applied_act) p.applied_act[m * kActPad + kAct] = 0.0f;
+            if (kDiag && p.dyn_noise_tape) p.dyn_noise_tape[m * kActPad + kAct] = 0.0f;
+        }
+        if (env_on) {
             double x;
             const uint32_t c = contacts8(jp, opd, size, finger, gbit, x);
             E8Reward& rw = RW[t & 1][eg];
@@ -474,9 +483,16 @@ __global__ __launch_bounds__(kE8Threads, 1) void k_pg_rollout_e8(PgRolloutArgs p
                 for (int j = 0; j < kJ; ++j)
                     if (jp[j] < 0.0f) nacc = nacc + jp[j];
                 rw.nacc[s] = nacc;
-                rw.x[s] = x;
             }
+            // dmin = min_f sqrt_rn(x_f) = sqrt_rn(min_f x_f) (the rounded root is monotone)
+            double xm = bcast8<0>(x);
+            const double x1 = bcast8<1>(x), x2 = bcast8<2>(x), x3 = bcast8<3>(x), x4 = bcast8<4>(x);
+            xm = x1 < xm ? x1 : xm;
+            xm = x2 < xm ? x2 : xm;
+            xm = x3 < xm ? x3 : xm;
+            xm = x4 < xm ? x4 : xm;
             if (s == 0) {
+                rw.dmin = sqrt(xm);
                 rw.c = c;
                 rw.prev = (flags & kHasPrev) ? ((flags >> kPrevShift) & 0xFFu) : 0x100u;
             }
@@ -521,43 +537,32 @@ __global__ __launch_bounds__(kE8Threads, 1) void k_pg_rollout_e8(PgRolloutArgs p
             ++rctr;
         }
         if (s == 0) RW[t & 1][eg].rctr = rctr;
-    };
-    // ---- aux lanes, P4: the policy sample, log pi(a|s) (gauss_logp's order), tapes
-    const auto aux_lane_step = [&](int64_t m) {
-        float term[kJ];
+        // log N(a | mu, sigma) terms of the finger's action dims (gauss_logp), off the step's
+        // chain (its own basic block after the reset); the aux twin sums them next step
+        __builtin_amdgcn_sched_barrier(0);
+        if (finger) {
 #pragma unroll
-        for (int j = 0; j < kJ; ++j) {
-            const int k = finger ? kJ * s + j : 0;
-            const float mu = mlp ? MU[eg * (kOut + 1) + k] : 0.0f;
-            const float a = mu + SIG[k] * DR.eps[16 * eg + k];
-            const float z = (a - mu) * ISIG[k];
-            term[j] = -0.5f * z * z - LS[k] - 0.5f * kLog2Pi;
-            if (finger) {
-                p.act[m * kActPad + k] = a;
-                if (kDiag && p.applied_act)
-                    p.applied_act[m * kActPad + k] = dyn_noise ? clipf(a + p.dyn_noise * DR.dzn[16 * eg + k], -1.0f, 1.0f) : a;
-                if (kDiag && p.dyn_noise_tape)
-                    p.dyn_noise_tape[m * kActPad + k] = dyn_noise ? p.dyn_noise * DR.dzn[16 * eg + k] : 0.0f;
+            for (int j = 0; j < kJ; ++j) {
+                const int k = kJ * s + j;
+                const float z = (a0[j] - mu0[j]) * ISIG[k];
+                RW[t & 1][eg].term[k] = -0.5f * z * z - LS[k] - 0.5f * kLog2Pi;
             }
         }
-        // the 15 terms summed in action order: lane f's three, f = 0..4 (row_sum_in_order's order)
+    };
+    // ---- aux lanes: log pi(a|s) of step t_ -- the env lanes' 15 terms summed in action order
+    // (gauss_logp / row_sum_in_order's order), one step after they were written
+    const auto settle_logp = [&](int64_t t_) {
+        const float4* tv = reinterpret_cast<const float4*>(RW[t_ & 1][eg].term);
         float lp = 0.0f;
 #pragma unroll
-        for (int j = 0; j < kJ; ++j) lp += bcast8<0>(term[j]);
-#pragma unroll
-        for (int j = 0; j < kJ; ++j) lp += bcast8<1>(term[j]);
-#pragma unroll
-        for (int j = 0; j < kJ; ++j) lp += bcast8<2>(term[j]);
-#pragma unroll
-        for (int j = 0; j < kJ; ++j) lp += bcast8<3>(term[j]);
-#pragma unroll
-        for (int j = 0; j < kJ; ++j) lp += bcast8<4>(term[j]);
-        if (s == 0) p.logp[m] = lp;
-        if (s == kF) {  // the tape's padding slot
-            p.act[m * kActPad + kAct] = 0.0f;
-            if (kDiag && p.applied_act) p.applied_act[m * kActPad + kAct] = 0.0f;
-            if (kDiag && p.dyn_noise_tape) p.dyn_noise_tape[m * kActPad + kAct] = 0.0f;
+        for (int q = 0; q < 4; ++q) {
+            const float4 v = tv[q];
+            lp += v.x;
+            lp += v.y;
+            lp += v.z;
+            if (4 * q + 3 < kAct) lp += v.w;
         }
+        if (s == 0) p.logp[t_ * n + i] = lp;
     };
 
     // diag & 128: s_memtime segment stamps per step: env waves into stamps[16 i + k], aux waves
@@ -620,14 +625,16 @@ __global__ __launch_bounds__(kE8Threads, 1) void k_pg_rollout_e8(PgRolloutArgs p
 #pragma unroll
             for (int q = 0; q < 4; ++q) MU[(16 * rt + 4 * g16 + q) * (kOut + 1) + r16] = acc[q] + b3_reg;
         }
-        if (aux) step_draws(ctr, t);
+        step_draws(ctr, t);
         E8_STAMP(3);
         lds_barrier();
         E8_STAMP(4);
         if (live) {
             if (aux) {
-                aux_lane_step(m);
-                if (t > 0 && env_on) settle(t - 1);  // step t-1's reward and bookkeeping
+                if (t > 0) {  // step t-1's log pi, reward and bookkeeping
+                    settle_logp(t - 1);
+                    if (env_on) settle(t - 1);
+                }
             } else {
                 env_lane_step(t, m);
             }
@@ -642,6 +649,7 @@ __global__ __launch_bounds__(kE8Threads, 1) void k_pg_rollout_e8(PgRolloutArgs p
         for (int q = 0; q < 8; ++q) p.stamps[16 * i + (aux ? 8 : 0) + q] = st_acc[q];
     }
     if (live && aux) {
+        if (T > 0) settle_logp(T - 1);
         if (T > 0 && env_on) settle(T - 1);
         if (kDiag && (p.diag & 2))
             for (int64_t t = 0; t < T && s == 0; ++t) p.rew[t * n + i] = 0.0f;
@@ -701,6 +709,20 @@ int launch_pg_rollout_e8(const PgRolloutArgs& p, int64_t n, bool noise, bool dia
                 fprintf(stderr, " s%d=%.0f", k, sum / n / p.horizon);
             }
             fprintf(stderr, "\n");
+            for (int wv = 0; wv < 4; ++wv) {  // per wave of the workgroup (envs 8 wv .. 8 wv + 7)
+                fprintf(stderr, "  wave %d:", 4 * w + wv);
+                for (int k = 0; k < 7; ++k) {
+                    double sum = 0;
+                    int64_t cnt = 0;
+                    for (int64_t e = 0; e < n; ++e)
+                        if ((e % kE8Envs) / 8 == wv) {
+                            sum += (double)h[e * 16 + 8 * w + k];
+                            ++cnt;
+                        }
+                    fprintf(stderr, " s%d=%.0f", k, cnt ? sum / cnt / p.horizon : 0.0);
+                }
+                fprintf(stderr, "\n");
+            }
         }
     }
     return DXRL_OK;

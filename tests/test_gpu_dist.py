@@ -56,7 +56,7 @@ def test_ranks_equal_one_rank_on_concatenated_batch(tmp_path, config, world):
     # every rank ends with the same parameters (identical Adam inputs after the all-reduce)
     for r in range(1, world):
         assert torch.equal(many[0]["params"], many[r]["params"]), r
-        assert torch.equal(many[0]["stats0"], many[r]["stats0"]), r
+        assert torch.equal(many[0]["stats0"][:5], many[r]["stats0"][:5]), r  # [5..7]: the rank's own moments
     # global advantage moments and normalisation == world 1 (f64, summation order only)
     for k in (0, 1, 2, 4):
         a, b = many[0]["stats0"][k].item(), one["stats0"][k].item()

@@ -44,9 +44,10 @@ __device__ __forceinline__ double clipd(double x, double lo, double hi) {
 struct u32x4 {
     uint32_t x, y, z, w;
 };
+template <int kRounds = 10>
 __device__ __forceinline__ u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < kRounds; ++r) {
         // each 32x32 -> 64-bit product as one v_mad_u64_u32 (both halves), not mul_lo + mul_hi
         const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
         const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
@@ -74,6 +75,13 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& n0, fl
     n0 = r * c;
     n1 = r * s;
 }
+
+// Rounds of the fused-noise streams (kStreamDyn, kStreamObs: config C5's robustness noise)
+#ifndef DXRL_NOISE_ROUNDS
+#define DXRL_NOISE_ROUNDS 10
+#endif
+constexpr int kNoiseRounds = DXRL_NOISE_ROUNDS;
+__device__ __forceinline__ u32x4 philox_noise(u32x4 c, uint32_t k0, uint32_t k1) { return philox<kNoiseRounds>(c, k0, k1); }
 
 // Stream ids for the Philox counter's third word.
 constexpr uint32_t kStreamReset = 0x52535400u, kStreamPolicy = 0x504f4c00u, kStreamDyn = 0x44594e00u,
@@ -409,7 +417,8 @@ __device__ __forceinline__ void store_env(const EnvSoA& s, int64_t i, const Env&
 
 // standard normal k of Philox block k / 4 (Box-Muller pairs (x, y), (z, w)), as philox_normals
 __device__ __forceinline__ float philox_normal_at(int k, uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream) {
-    const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)(k >> 2)}, k0, k1);
+    const u32x4 c = u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)(k >> 2)};
+    const u32x4 r = stream == kStreamPolicy ? philox(c, k0, k1) : philox_noise(c, k0, k1);
     float n0, n1;  // operands selected first: one branch-free Box-Muller (schedulable into MFMA gaps)
     const bool hi = (k & 2) != 0;
     box_muller(hi ? r.z : r.x, hi ? r.w : r.y, n0, n1);

@@ -50,6 +50,13 @@ int launch_wgrad(const bf16* Y, int64_t ldy, int O, const bf16* X, int64_t ldx, 
 int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, const bf16* W1, int64_t M,
                     int splits, float* partial, float* out, hipStream_t st, int64_t ldo, int reduce = 1,
                     int* nslabs = nullptr);
+// Both networks' dW2 in one launch (same observation rows, same M): splits0 workgroups run the
+// first contraction, splits1 the second, each split exactly as a single launch_wgrad_l1 with that
+// split count would run it (so each net's partial slabs are that launch's); the partials are left
+// for the caller to sum (*nslabs0 / *nslabs1 slabs).
+int launch_wgrad_l1_pair(const bf16* Y0, const bf16* W10, int splits0, float* partial0, float* out0, const bf16* Y1,
+                         const bf16* W11, int splits1, float* partial1, float* out1, int64_t ldy, const bf16* obs,
+                         int64_t ldobs, int64_t M, int64_t ldo, hipStream_t st, int* nslabs0, int* nslabs1);
 
 // s += partial[k * stride4 + i] for k = k0 .. k1 - 1, in that order, with the loads issued in
 // batches of 8 ahead of their adds (the plain loop waits out one load latency per slab: the

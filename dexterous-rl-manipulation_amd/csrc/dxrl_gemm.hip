@@ -647,13 +647,24 @@ __device__ __forceinline__ void wait_chunks(int n) { wait_chunks_k<3>(n); }
 
 // kDiag: the DXRL_WGRAD_DIAG ablations compiled in (a run-time branch in the chunk loop costs the
 // production kernel measurable time)
+// Two contractions in one launch (both networks' dW2 of a PPO step): workgroups [0, nb0) run n[0]
+// over nb0 splits, the rest n[1] over gridDim.x - nb0; a single contraction sets nb0 = gridDim.x.
+struct WgradPair {
+    WgradArgs n[2];
+    int nb0;
+};
 template <bool kDiag>
-__global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
+__global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradPair pr) {
     extern __shared__ __attribute__((aligned(16))) char gsm[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
+    const bool second = (int)blockIdx.x >= pr.nb0;
+    const WgradArgs& w = second ? pr.n[1] : pr.n[0];
+    // this workgroup's split of its contraction and the contraction's split count
+    const int bx = second ? (int)blockIdx.x - pr.nb0 : (int)blockIdx.x;
+    const int gx = second ? (int)gridDim.x - pr.nb0 : pr.nb0;
     const int64_t total = w.M / kLK;
-    const int nch = (int)((total - blockIdx.x + gridDim.x - 1) / gridDim.x);
+    const int nch = (int)((total - bx + gx - 1) / gx);
     const bf16* const Y = w.Y;
     const bf16* const X = w.X;
     const int64_t ldy = w.ldy, ldx = w.ldx;
@@ -678,7 +689,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
         if (!dma_wave) return;
         const int q = wave & 3;
         char* slot = gsm + (c % kLNB) * kLSlot;
-        const int64_t m0 = ((int64_t)blockIdx.x + (int64_t)c * gridDim.x) * kLK;
+        const int64_t m0 = ((int64_t)bx + (int64_t)c * gx) * kLK;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {  // dH2 rows 8 q + 2 i, + 1
             const int prow = 8 * q + 2 * i;
@@ -694,7 +705,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
     const auto wait_in = [](int n) { wait_chunks(n); };
     const auto issue = [&](int c) {
         char* slot = gsm + (c % kLNB) * kLSlot;
-        const int64_t m0 = ((int64_t)blockIdx.x + (int64_t)c * gridDim.x) * kLK;
+        const int64_t m0 = ((int64_t)bx + (int64_t)c * gx) * kLK;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {  // dH2 rows 4 wave + 2 i, + 1
             const int prow = 4 * wave + 2 * i;
@@ -771,7 +782,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
         __builtin_amdgcn_sched_barrier(0);
         if (next) recompute_store(c + 1, ha);
     }
-    float* dst = w.partial ? w.partial + (int64_t)blockIdx.x * 256 * 256 : w.out;
+    float* dst = w.partial ? w.partial + (int64_t)bx * 256 * 256 : w.out;
     const int64_t ld = w.partial ? 256 : w.ldo;
     if (kDiag && (w.diag & 4)) return;  // ablation: no partial-slab stores
 #pragma unroll
@@ -782,14 +793,15 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradArgs w) {
     }
 }
 
-int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, const bf16* W1, int64_t M,
-                    int splits, float* partial, float* out, hipStream_t st, int64_t ldo, int reduce, int* nslabs) {
+namespace {
+int wgrad_l1_args(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, const bf16* W1, int64_t M, int& splits,
+                  float* partial, float* out, int64_t ldo, WgradArgs& w) {
     DXRL_REQUIRE(Y && obs && W1 && out && M > 0 && M % kLK == 0, "wgrad_l1: M must be a positive multiple of %d", kLK);
     DXRL_REQUIRE(ldy >= 256 && ldy % 8 == 0 && ldobs >= 64 && ldobs % 8 == 0 && ldo >= 256, "wgrad_l1: bad strides");
     if (splits < 1) splits = 1;
     if (splits > M / kLK) splits = (int)(M / kLK);
     if (splits > 1) DXRL_REQUIRE(partial, "wgrad_l1: split-K needs a partial slab");
-    WgradArgs w{};
+    w = WgradArgs{};
     w.Y = Y;
     w.ldy = ldy;
     w.X = obs;
@@ -801,6 +813,9 @@ int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, 
     w.out = out;
     w.partial = splits > 1 ? partial : nullptr;
     w.ldo = ldo;
+    return DXRL_OK;
+}
+int wgrad_l1_launch(const WgradPair& pr, int grid, hipStream_t st) {
     static bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void*>(k_wgrad_l1<false>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, kLLds) == hipSuccess &&
@@ -812,10 +827,34 @@ int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, 
         const char* v = getenv("DXRL_WGRAD_DIAG");
         return v ? atoi(v) : 0;
     }();
-    w.diag = diag;
-    if (diag) hipLaunchKernelGGL(k_wgrad_l1<true>, dim3((unsigned)splits), dim3(512), kLLds, st, w);
-    else hipLaunchKernelGGL(k_wgrad_l1<false>, dim3((unsigned)splits), dim3(512), kLLds, st, w);
-    if (int rc = launch_check("k_wgrad_l1")) return rc;
+    WgradPair p = pr;
+    p.n[0].diag = p.n[1].diag = diag;
+    if (diag) hipLaunchKernelGGL(k_wgrad_l1<true>, dim3((unsigned)grid), dim3(512), kLLds, st, p);
+    else hipLaunchKernelGGL(k_wgrad_l1<false>, dim3((unsigned)grid), dim3(512), kLLds, st, p);
+    return launch_check("k_wgrad_l1");
+}
+}  // namespace
+
+int launch_wgrad_l1_pair(const bf16* Y0, const bf16* W10, int splits0, float* partial0, float* out0, const bf16* Y1,
+                         const bf16* W11, int splits1, float* partial1, float* out1, int64_t ldy, const bf16* obs,
+                         int64_t ldobs, int64_t M, int64_t ldo, hipStream_t st, int* nslabs0, int* nslabs1) {
+    WgradPair pr{};
+    if (int rc = wgrad_l1_args(Y0, ldy, obs, ldobs, W10, M, splits0, partial0, out0, ldo, pr.n[0])) return rc;
+    if (int rc = wgrad_l1_args(Y1, ldy, obs, ldobs, W11, M, splits1, partial1, out1, ldo, pr.n[1])) return rc;
+    pr.nb0 = splits0;
+    if (int rc = wgrad_l1_launch(pr, splits0 + splits1, st)) return rc;
+    *nslabs0 = splits0 > 1 ? splits0 : 0;
+    *nslabs1 = splits1 > 1 ? splits1 : 0;
+    return DXRL_OK;
+}
+
+int launch_wgrad_l1(const bf16* Y, int64_t ldy, const bf16* obs, int64_t ldobs, const bf16* W1, int64_t M,
+                    int splits, float* partial, float* out, hipStream_t st, int64_t ldo, int reduce, int* nslabs) {
+    WgradPair pr{};
+    if (int rc = wgrad_l1_args(Y, ldy, obs, ldobs, W1, M, splits, partial, out, ldo, pr.n[0])) return rc;
+    pr.n[1] = pr.n[0];
+    pr.nb0 = splits;
+    if (int rc = wgrad_l1_launch(pr, splits, st)) return rc;
     if (nslabs) *nslabs = splits > 1 ? splits : 0;
     if (splits > 1 && reduce) {
         const int64_t slab = 256 * 256;

@@ -39,7 +39,8 @@ template <int N>
 __device__ __forceinline__ void philox_normals(float* out, uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream) {
 #pragma unroll
     for (int b = 0; b < (N + 3) / 4; ++b) {
-        const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)b}, k0, k1);
+        const u32x4 c = u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)b};
+        const u32x4 r = stream == kStreamPolicy ? philox(c, k0, k1) : philox_noise(c, k0, k1);
         float n0, n1, n2, n3;
         box_muller(r.x, r.y, n0, n1);
         box_muller(r.z, r.w, n2, n3);
@@ -74,7 +75,7 @@ __device__ __forceinline__ void write_policy_obs(const Env& e, bf16* xrow, float
     for (int b = 0; b < (kObs + 3) / 4; ++b) {
         float nz[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         if (obs_noise > 0.0f) {
-            const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamObs, (uint32_t)b}, k0, k1);
+            const u32x4 r = philox_noise(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamObs, (uint32_t)b}, k0, k1);
             box_muller(r.x, r.y, nz[0], nz[1]);
             box_muller(r.z, r.w, nz[2], nz[3]);
         }
@@ -863,7 +864,8 @@ constexpr int kWsWaves = 8, kWsThreads = 64 * kWsWaves;
 // row parity (row t + 1's is written in step t's P0 while the env lanes read row t's).  The reward inputs (WsReward) are double-buffered
 // by step parity: the env lanes write step t's while the aux lanes settle step t-1's.
 struct __attribute__((aligned(16))) WsDraws {
-    float eps[256], dzn[256], on[2][4][256];  // on: double-buffered by observation row parity
+    // on: the observation noise, double-buffered by row parity, element k of env e at [e][k]
+    float eps[256], dzn[256], on[2][kLsEnvs * 48];
     double u1[256], u2[256];
 };
 // one env lane's extra reset draw (config.py:44-113 samplers): lo + span u with a range, the
@@ -1046,26 +1048,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     // dynamics-noise block s - 11 (normals 4(s-11) .. +3); lanes 0..11 observation-noise block s
     // (obs elements 4s .. 4s + 3).  Same blocks and arithmetic as philox_normal_at /
     // reset_uniform_at, so the values are identical.
-    const auto obs_slot = [&](int k, int& ln, int& j) {  // inverse of row_obs_elem
-        if (k < kD) {
-            ln = k;
-            j = 0;
-        } else if (k < 2 * kD) {
-            ln = k - kD;
-            j = 1;
-        } else if (k < 2 * kD + 7) {
-            ln = k - 2 * kD;
-            j = 2;
-        } else if (k < 2 * kD + 10) {
-            ln = k - 2 * kD - 7;
-            j = 3;
-        } else {
-            ln = 7 + (k - 2 * kD - 10);
-            j = 2;
-        }
-    };
-    const auto normals4 = [&](uint64_t ctr, uint32_t stream, int blk, float nz[4]) {
-        const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)blk}, pk0, pk1);
+    const auto normals4 = [&](uint64_t ctr, uint32_t stream, int blk, float nz[4]) {  // noise streams only
+        const u32x4 r = philox_noise(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)blk}, pk0, pk1);
         box_muller(r.x, r.y, nz[0], nz[1]);
         box_muller(r.z, r.w, nz[2], nz[3]);
     };
@@ -1135,15 +1119,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
             *reinterpret_cast<float4*>(&DR.dzn[rbase + 4 * (s - kOb)]) = float4{nz[0], nz[1], nz[2], nz[3]};
             return;
         }
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const int k = 4 * s + h;
-            if (k < kObs) {
-                int ln, j;
-                obs_slot(k, ln, j);
-                DR.on[buf][j][rbase + ln] = nz[h];
-            }
-        }
+        // elements 4 s .. 4 s + 3 of the env's row (45..47 never read): one 16-byte store
+        *reinterpret_cast<float4*>(&DR.on[buf][48 * eg + 4 * s]) = float4{nz[0], nz[1], nz[2], nz[3]};
         if (kDiag && p.obs_noise_tape) {  // parity tape: the value write_obs_row adds (row ctr - iteration T)
             const int64_t row = (int64_t)(ctr - p.iteration * (uint64_t)T);
             float4 v;
@@ -1196,7 +1173,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     const auto write_obs_row = [&](int buf) {  // buf: the row's noise buffer (row parity)
         bf16* xr = X + eg * kXsW;
         const auto put = [&](int j, float v, int k) {
-            if (obs_noise) v = v + p.obs_noise * DR.on[buf][j][et_tid];
+            (void)j;
+            if (obs_noise) v = v + p.obs_noise * DR.on[buf][48 * eg + k];
             xr[k] = to_bf16(v);
         };
         const float v2 = s < 3 ? (float)opd : (s < 7 ? (s == 3 ? 1.0f : 0.0f) : (float)((flags >> ((s - 7) & 31)) & 1u));

@@ -1256,6 +1256,28 @@ __global__ __launch_bounds__(256) void k_grad_reduce_pair(const float4* __restri
     else slab_reduce_block(wpart, (int64_t)kH * kH / 4, wz, gW2, 0, kH, ldo, (int64_t)blockIdx.x - nb1, grp);
 }
 
+// Both networks' reductions of a paired learner step in one launch: blocks [0, nbA) are net A's
+// k_grad_reduce_pair blocks, the rest net B's -- each element summed in the order its own pass's
+// reduction would use.
+struct GradReduceNet {
+    const float4* fpart;
+    int fz;
+    float *gW1, *gW3, *gLs, *gW2;
+    float ent_coef;
+    const float4* wpart;
+    int wz;
+    int64_t ldo;
+    int nb1, nb2;
+};
+__global__ __launch_bounds__(256) void k_grad_reduce_nets(GradReduceNet a, GradReduceNet b) {
+    __shared__ float4 grp[kReduceGroups][16];
+    const bool second = (int)blockIdx.x >= a.nb1 + a.nb2;
+    const GradReduceNet& r = second ? b : a;
+    const int64_t blk = second ? (int64_t)blockIdx.x - (a.nb1 + a.nb2) : (int64_t)blockIdx.x;
+    if (blk < r.nb1) fused_reduce_block(r.fpart, r.fz, r.gW1, r.gW3, r.gLs, r.gW2, r.ent_coef, blk, grp);
+    else slab_reduce_block(r.wpart, (int64_t)kH * kH / 4, r.wz, r.gW2, 0, kH, r.ldo, blk - r.nb1, grp);
+}
+
 // grads blocks W1 / W3 (and log_std for the actor) from the workgroup sum (launch_slab_reduce)
 __global__ void k_fused_scatter(const float* __restrict__ sum, float* __restrict__ gW1, float* __restrict__ gW3,
                                 float* __restrict__ gLs, float* __restrict__ gW2, float ent_coef) {
@@ -1277,6 +1299,17 @@ int dxrl_pg_fused_sizes(int32_t* tile_rows, int64_t* partial_floats_per_block) {
     return DXRL_OK;
 }
 
+}  // extern "C"
+
+namespace dxrl {
+namespace {
+// k_pg_fused itself (no dW2 contraction, no reductions); the grid it ran in *grid_out
+int fused_kernel(const dxrl_pg_fused_args* a, hipStream_t st, int* grid_out);
+}  // namespace
+}  // namespace dxrl
+
+extern "C" {
+
 int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     DXRL_REQUIRE(a && a->packed && a->params && a->obs && a->rows > 0, "fused: null arguments");
     DXRL_REQUIRE(a->net == 0 || a->net == 1, "fused: net must be 0 (actor) or 1 (critic)");
@@ -1295,6 +1328,117 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
     DXRL_REQUIRE((reinterpret_cast<uintptr_t>(a->obs) & 15) == 0, "fused: obs must be 16-byte aligned");
     DeviceGuard g(device);
     hipStream_t st = as_stream(stream);
+    int grid = 0;
+    if (int rc = fused_kernel(a, st, &grid)) return rc;
+    if (!train) return DXRL_OK;
+    const bf16* w = static_cast<const bf16*>(a->packed);
+    const bool c = a->net == 1;
+    const int64_t o2 = c ? kOffW2c : kOffW2a, o3 = c ? kOffW3c : kOffW3a;
+    const bool recompute = a->rows % 32 == 0 && a->h1_mode == 0;
+    float* G = a->grads;
+    // the pad columns 257..287 of the W3 slab are never written: the scatter zeroes them
+    float* tmp = a->partial + (int64_t)grid * kPartSize;
+    float* sum = tmp + (int64_t)kReduceGroups * kPartSize;
+    const bool aligned = (reinterpret_cast<uintptr_t>(a->partial) & 15) == 0;
+    if (aligned && recompute && (reinterpret_cast<uintptr_t>(a->wgrad_partial) & 15) == 0 &&
+        (reinterpret_cast<uintptr_t>(G + o2) & 15) == 0) {
+        // dW2 first (its partials only), then both reductions in one launch
+        int ns = 0;
+        if (int rc = launch_wgrad_l1(static_cast<const bf16*>(a->dh2), kH, static_cast<const bf16*>(a->obs), kIn,
+                                     w + (c ? kBfW1c : kBfW1a), a->rows, a->wgrad_splits, a->wgrad_partial, G + o2, st,
+                                     kHx, 0, &ns))
+            return rc;
+        const int nb1 = (int)((kPartSize / 4 + 15) / 16);
+        int nb2 = 0;
+        if (ns > kReduceGroups) {
+            nb2 = kH * kH / 4 / 16;
+        } else if (ns > 0) {  // few slabs: the one-level sum (k_slab_reduce2_4 is the two-level form)
+            if (int rc = launch_slab_reduce(a->wgrad_partial, (int64_t)kH * kH, ns, nullptr, G + o2, 0, st, kH, kHx))
+                return rc;
+        }
+        hipLaunchKernelGGL(k_grad_reduce_pair, dim3((unsigned)(nb1 + nb2)), dim3(256), 0, st,
+                           reinterpret_cast<const float4*>(a->partial), grid, G + (c ? kOffW1c : kOffW1a), G + o3,
+                           c ? nullptr : G + kOffLogStd, G + o2, (float)a->ent_coef,
+                           reinterpret_cast<const float4*>(a->wgrad_partial), ns, (int64_t)kHx, nb1);
+        return launch_check("k_grad_reduce_pair");
+    }
+    if (aligned) {
+        (void)tmp;
+        (void)sum;
+        hipLaunchKernelGGL(k_fused_reduce_scatter, dim3((unsigned)((kPartSize / 4 + 15) / 16)), dim3(256), 0, st,
+                           reinterpret_cast<const float4*>(a->partial), grid, G + (c ? kOffW1c : kOffW1a), G + o3,
+                           c ? nullptr : G + kOffLogStd, G + o2, (float)a->ent_coef);
+        if (int rc = launch_check("k_fused_reduce_scatter")) return rc;
+    } else {
+        if (int rc = launch_slab_reduce(a->partial, kPartSize, grid, tmp, sum, 0, st)) return rc;
+        hipLaunchKernelGGL(k_fused_scatter, dim3((kPartSize + 255) / 256), dim3(256), 0, st, sum,
+                           G + (c ? kOffW1c : kOffW1a), G + o3, c ? nullptr : G + kOffLogStd, G + o2,
+                           (float)a->ent_coef);
+        if (int rc = launch_check("k_fused_scatter")) return rc;
+    }
+    // dW2[:, 0..255] = dH2^T H1 (the bias column 256 came from the column sums above)
+    if (recompute)
+        return launch_wgrad_l1(static_cast<const bf16*>(a->dh2), kH, static_cast<const bf16*>(a->obs), kIn,
+                               w + (c ? kBfW1c : kBfW1a), a->rows, a->wgrad_splits, a->wgrad_partial, G + o2, st, kHx);
+    return launch_wgrad(static_cast<const bf16*>(a->dh2), kH, kH, static_cast<const bf16*>(a->h1), kHx, kH, a->rows,
+                        a->wgrad_splits, a->wgrad_partial, G + o2, st, kHx);
+}
+
+int dxrl_pg_fused_pair(int32_t device, const dxrl_pg_fused_args* c, const dxrl_pg_fused_args* a, void* stream) {
+    DXRL_REQUIRE(c && a, "fused_pair: null arguments");
+    DXRL_REQUIRE(c->net == 1 && a->net == 0 && c->train && a->train, "fused_pair: a critic and an actor train pass");
+    DXRL_REQUIRE(c->rows == a->rows && c->rows > 0 && c->rows % 32 == 0 && c->obs == a->obs && c->packed == a->packed &&
+                     c->grads == a->grads && c->params == a->params,
+                 "fused_pair: both passes over the same samples, weights and gradient buffer (rows % 32 == 0)");
+    DXRL_REQUIRE(c->h1_mode == 0 && a->h1_mode == 0, "fused_pair: H1 recomputed on chip (h1_mode 0)");
+    DXRL_REQUIRE(c->dh2 && a->dh2 && c->dh2 != a->dh2 && c->partial && a->partial && c->partial != a->partial &&
+                     c->wgrad_partial && a->wgrad_partial && c->wgrad_partial != a->wgrad_partial,
+                 "fused_pair: each pass needs its own dh2, partial and wgrad_partial buffers");
+    DXRL_REQUIRE(c->wgrad_splits > kReduceGroups && a->wgrad_splits > kReduceGroups,
+                 "fused_pair: wgrad_splits > %d per network", kReduceGroups);
+    DXRL_REQUIRE(c->act == nullptr || (reinterpret_cast<uintptr_t>(c->act) & 15) == 0, "fused_pair: alignment");
+    for (const dxrl_pg_fused_args* x : {c, a}) {
+        DXRL_REQUIRE(x->packed && x->params && x->obs && x->loss_partial && x->grid >= 1 && x->grid <= 65535,
+                     "fused_pair: null arguments");
+        DXRL_REQUIRE(x->net == 1 ? (x->ret != nullptr) : (x->act && x->logp_old && x->adv && x->stats),
+                     "fused_pair: missing head inputs");
+        DXRL_REQUIRE(((reinterpret_cast<uintptr_t>(x->partial) | reinterpret_cast<uintptr_t>(x->wgrad_partial) |
+                       reinterpret_cast<uintptr_t>(x->obs) | reinterpret_cast<uintptr_t>(x->act)) & 15) == 0,
+                     "fused_pair: partial / wgrad_partial / obs / act must be 16-byte aligned");
+    }
+    DeviceGuard g(device);
+    hipStream_t st = as_stream(stream);
+    int grid_c = 0, grid_a = 0;
+    if (int rc = fused_kernel(c, st, &grid_c)) return rc;
+    if (int rc = fused_kernel(a, st, &grid_a)) return rc;
+    const bf16* w = static_cast<const bf16*>(a->packed);
+    float* G = a->grads;
+    int ns_c = 0, ns_a = 0;
+    // both dW2 contractions in one launch (their split counts side by side on the CUs), then both
+    // networks' reductions in one launch
+    if (int rc = launch_wgrad_l1_pair(static_cast<const bf16*>(c->dh2), w + kBfW1c, c->wgrad_splits, c->wgrad_partial,
+                                      G + kOffW2c, static_cast<const bf16*>(a->dh2), w + kBfW1a, a->wgrad_splits,
+                                      a->wgrad_partial, G + kOffW2a, kH, static_cast<const bf16*>(a->obs), kIn, a->rows,
+                                      kHx, st, &ns_c, &ns_a))
+        return rc;
+    DXRL_REQUIRE(ns_c > kReduceGroups && ns_a > kReduceGroups, "fused_pair: too few rows for the splits");
+    const int nb1 = (int)((kPartSize / 4 + 15) / 16), nb2 = kH * kH / 4 / 16;
+    GradReduceNet rc_{reinterpret_cast<const float4*>(c->partial), grid_c, G + kOffW1c, G + kOffW3c, nullptr,
+                      G + kOffW2c, (float)c->ent_coef, reinterpret_cast<const float4*>(c->wgrad_partial), ns_c,
+                      (int64_t)kHx, nb1, nb2};
+    GradReduceNet ra_{reinterpret_cast<const float4*>(a->partial), grid_a, G + kOffW1a, G + kOffW3a, G + kOffLogStd,
+                      G + kOffW2a, (float)a->ent_coef, reinterpret_cast<const float4*>(a->wgrad_partial), ns_a,
+                      (int64_t)kHx, nb1, nb2};
+    hipLaunchKernelGGL(k_grad_reduce_nets, dim3((unsigned)(2 * (nb1 + nb2))), dim3(256), 0, st, rc_, ra_);
+    return launch_check("k_grad_reduce_nets");
+}
+
+}  // extern "C"
+
+namespace dxrl {
+namespace {
+int fused_kernel(const dxrl_pg_fused_args* a, hipStream_t st, int* grid_out) {
+    const bool train = a->train != 0;
     const bf16* w = static_cast<const bf16*>(a->packed);
     const bool c = a->net == 1;
     const int64_t o2 = c ? kOffW2c : kOffW2a, o3 = c ? kOffW3c : kOffW3a;
@@ -1336,8 +1480,9 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
         const char* v = getenv("DXRL_FUSED_TILE");
         return v && atoi(v) == 64 ? 64 : 128;
     }();
-    static const int cus = [device] {
-        int n = 0;
+    static const int cus = [] {
+        int n = 0, device = 0;
+        (void)hipGetDevice(&device);  // the caller's DeviceGuard made it current
         return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0 ? n
                                                                                                             : 256;
     }();
@@ -1384,53 +1529,8 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
         }
         fprintf(stderr, "\n");
     }
-    if (!train) return DXRL_OK;
-    float* G = a->grads;
-    // the pad columns 257..287 of the W3 slab are never written: the scatter zeroes them
-    float* tmp = a->partial + (int64_t)grid * kPartSize;
-    float* sum = tmp + (int64_t)kReduceGroups * kPartSize;
-    const bool aligned = (reinterpret_cast<uintptr_t>(a->partial) & 15) == 0;
-    if (aligned && recompute && (reinterpret_cast<uintptr_t>(a->wgrad_partial) & 15) == 0 &&
-        (reinterpret_cast<uintptr_t>(G + o2) & 15) == 0) {
-        // dW2 first (its partials only), then both reductions in one launch
-        int ns = 0;
-        if (int rc = launch_wgrad_l1(static_cast<const bf16*>(a->dh2), kH, f.X, kIn, w + (c ? kBfW1c : kBfW1a), a->rows,
-                                     a->wgrad_splits, a->wgrad_partial, G + o2, st, kHx, 0, &ns))
-            return rc;
-        const int nb1 = (int)((kPartSize / 4 + 15) / 16);
-        int nb2 = 0;
-        if (ns > kReduceGroups) {
-            nb2 = kH * kH / 4 / 16;
-        } else if (ns > 0) {  // few slabs: the one-level sum (k_slab_reduce2_4 is the two-level form)
-            if (int rc = launch_slab_reduce(a->wgrad_partial, (int64_t)kH * kH, ns, nullptr, G + o2, 0, st, kH, kHx))
-                return rc;
-        }
-        hipLaunchKernelGGL(k_grad_reduce_pair, dim3((unsigned)(nb1 + nb2)), dim3(256), 0, st,
-                           reinterpret_cast<const float4*>(a->partial), grid, G + (c ? kOffW1c : kOffW1a), G + o3,
-                           c ? nullptr : G + kOffLogStd, G + o2, (float)a->ent_coef,
-                           reinterpret_cast<const float4*>(a->wgrad_partial), ns, (int64_t)kHx, nb1);
-        return launch_check("k_grad_reduce_pair");
-    }
-    if (aligned) {
-        (void)tmp;
-        (void)sum;
-        hipLaunchKernelGGL(k_fused_reduce_scatter, dim3((unsigned)((kPartSize / 4 + 15) / 16)), dim3(256), 0, st,
-                           reinterpret_cast<const float4*>(a->partial), grid, G + (c ? kOffW1c : kOffW1a), G + o3,
-                           c ? nullptr : G + kOffLogStd, G + o2, (float)a->ent_coef);
-        if (int rc = launch_check("k_fused_reduce_scatter")) return rc;
-    } else {
-        if (int rc = launch_slab_reduce(a->partial, kPartSize, grid, tmp, sum, 0, st)) return rc;
-        hipLaunchKernelGGL(k_fused_scatter, dim3((kPartSize + 255) / 256), dim3(256), 0, st, sum,
-                           G + (c ? kOffW1c : kOffW1a), G + o3, c ? nullptr : G + kOffLogStd, G + o2,
-                           (float)a->ent_coef);
-        if (int rc = launch_check("k_fused_scatter")) return rc;
-    }
-    // dW2[:, 0..255] = dH2^T H1 (the bias column 256 came from the column sums above)
-    if (recompute)
-        return launch_wgrad_l1(static_cast<const bf16*>(a->dh2), kH, f.X, kIn, w + (c ? kBfW1c : kBfW1a), a->rows,
-                               a->wgrad_splits, a->wgrad_partial, G + o2, st, kHx);
-    return launch_wgrad(static_cast<const bf16*>(a->dh2), kH, kH, static_cast<const bf16*>(a->h1), kHx, kH, a->rows,
-                        a->wgrad_splits, a->wgrad_partial, G + o2, st, kHx);
+    *grid_out = grid;
+    return DXRL_OK;
 }
-
-}  // extern "C"
+}  // namespace
+}  // namespace dxrl

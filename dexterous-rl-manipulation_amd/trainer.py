@@ -93,6 +93,11 @@ class TrainerConfig:
     # (overlap_comm); 0 = every CU.  Changes the learner's per-workgroup partial-sum order (so the
     # gradients' last bits), not the sums themselves; overlapped == serialised holds at any value.
     reserve_cus: int = 0
+    # both train passes of a step through dxrl_pg_fused_pair: their dW2 contractions in one launch
+    # (learner CUs / 2 splits each instead of every CU per network: half the split-K slab traffic)
+    # and both reductions in one launch (needs the fused learner with on-chip H1, serialised
+    # exchanges, and > 16 row chunks per split); False: one dxrl_pg_fused call per network
+    pair_learner: bool = True
 
 
 def minibatch_bounds(M: int, B: int, round_samples: int):
@@ -236,6 +241,18 @@ class PGTrainer:
         self.fused_grid = 2 * cus if self.learner_cus == cus else self.learner_cus
         self.fused_partial = z(self.fused_grid + 17, pf_.value)  # + reduction scratch and sum
         self.fused_loss = torch.zeros(self.fused_grid, 4, dtype=torch.float64, device=d)
+        # paired learner step (dxrl_pg_fused_pair): the critic's own dH2 / partial buffers, the
+        # per-network dW2 split count (every minibatch slice must give each split > 16 chunks)
+        mb_rows = min(b - a for a, b in zip(self.minibatch_bounds()[:-1], self.minibatch_bounds()[1:]))
+        self.pair_splits = min(self.learner_cus // 2, mb_rows // 32)
+        self.paired = (cfg.pair_learner and cfg.fused and cfg.h1_recompute and self._comm is None
+                       and self.pair_splits > 16 and all(x % 32 == 0 for x in self.minibatch_bounds()))
+        self.dH2c = self.fused_partial_c = self.kpartial_c = self.kpartial_a = None
+        if self.paired:
+            self.dH2c = z(M, H, dt=bf)
+            self.fused_partial_c = z(self.fused_grid + 17, pf_.value)
+            self.kpartial_a = z(self.pair_splits, H, H)
+            self.kpartial_c = z(self.pair_splits, H, H)
         self.pack()
 
     # ------------------------------------------------------------------ params
@@ -336,6 +353,21 @@ class PGTrainer:
         f.h1_mode = 0 if c.h1_recompute else 1
         return f
 
+    def train(self):
+        """Both train passes of the step (critic, then actor) with their dW2 contractions in one
+        launch and both networks' reductions in one launch (dxrl_pg_fused_pair)."""
+        start, rows = self._mb
+        self._loss_rows = rows
+        if self._stats_pending:
+            torch.cuda.current_stream(self.dev).wait_event(self._stats_event)
+            self._stats_pending = False
+        fc, fa = self._fused_args(1, True, rows, start), self._fused_args(0, True, rows, start)
+        p = N.ptr
+        fc.dh2, fc.partial, fc.wgrad_partial = p(self.dH2c), p(self.fused_partial_c), p(self.kpartial_c)
+        fa.wgrad_partial = p(self.kpartial_a)
+        fc.wgrad_splits = fa.wgrad_splits = self.pair_splits
+        N.call("dxrl_pg_fused_pair", self.dev.index, C.byref(fc), C.byref(fa), self._s())
+
     def critic_values(self):
         """V over the T + 1 observation blocks (fused forward, nothing stored but V)."""
         N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(1, False, self.M + self.n)), self._s())
@@ -372,10 +404,17 @@ class PGTrainer:
         for _ in range(c.epochs):
             for k in rng.permutation(c.minibatches):
                 self._mb = (bounds[k], bounds[k + 1] - bounds[k])
-                self.critic_train()
-                self.actor_train()
+                self.train_passes()
                 self.optimizer_step()
         self._mb = (0, self.M)
+
+    def train_passes(self):
+        """The step's two train passes: paired (train) or one call per network."""
+        if self.paired:
+            self.train()
+        else:
+            self.critic_train()
+            self.actor_train()
 
     def minibatch_bounds(self):
         return minibatch_bounds(self.M, self.cfg.minibatches, 128 * self.learner_cus)
@@ -384,6 +423,8 @@ class PGTrainer:
         """The iteration's launch groups in order (bench.py times each)."""
         if self.cfg.fused and self.cfg.epochs * self.cfg.minibatches > 1:
             ph = ["rollout", "critic_values", "advantages", "ppo_updates"]
+        elif self.cfg.fused and self.paired:
+            ph = ["rollout", "critic_values", "advantages", "train", "optimizer_step"]
         elif self.cfg.fused:
             # the critic first: its pass does not need the (all-gathered) normalisation moments
             ph = ["rollout", "critic_values", "advantages", "critic_train", "actor_train", "optimizer_step"]
@@ -634,8 +675,7 @@ class PGTrainer:
             for name in self.phases():
                 with profiling.range_(f"pg.{name}") if marks else _null():
                     if name == "ppo_updates" and not update:
-                        self.critic_train()
-                        self.actor_train()
+                        self.train_passes()
                     elif name != "optimizer_step" or update:
                         getattr(self, name)()
         finally:

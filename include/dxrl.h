@@ -479,6 +479,14 @@ typedef struct dxrl_pg_fused_args {
 
 int dxrl_pg_fused_sizes(int32_t* tile_rows, int64_t* partial_floats_per_block);
 int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* args, void* stream);
+/* Both train passes of one learner step (a PPO minibatch, or the whole batch) with their
+ * dW2 contractions in ONE k_wgrad_l1 launch (critic->wgrad_splits + actor->wgrad_splits
+ * workgroups side by side) and every reduction of both networks in ONE launch.  Same
+ * per-network arithmetic as two dxrl_pg_fused calls with those split counts; each pass needs
+ * its own dh2 / partial / wgrad_partial buffers, h1_mode 0, rows % 32 == 0, splits > 16.
+ * No reference counterpart (policies/simple_learner.py:73-95 is the update it replaces). */
+int dxrl_pg_fused_pair(int32_t device, const dxrl_pg_fused_args* critic, const dxrl_pg_fused_args* actor,
+                       void* stream);
 
 /* ------------------------------------------------------------------------
  * Evaluation episode programs:

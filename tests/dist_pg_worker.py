@@ -5,7 +5,7 @@ iterations (rollout, GAE with the global advantage moments, fused learner, gradi
 all-reduce, Adam) and saves what the test compares against the world-1 run on the
 concatenated batch.
 
-    python tests/dist_pg_worker.py OUT.pt N_LOCAL ITERS CONFIG [OVERLAP 1|0]   (RANK / WORLD_SIZE / MASTER_* in env)
+    python tests/dist_pg_worker.py OUT.pt N_LOCAL ITERS CONFIG [MODE 0|1|u]   (RANK / WORLD_SIZE / MASTER_* in env)
 """
 import os
 import sys
@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(out, n, iters, config, overlap=True):
+def run(out, n, iters, config, overlap="0"):
     import torch
     import dexterous_rl_manipulation_amd as pkg
     from dexterous_rl_manipulation_amd import distributed as D, envs, trainer
@@ -30,8 +30,11 @@ def run(out, n, iters, config, overlap=True):
     cur = {"default": "easy"}.get(config, config)
     env = envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.named(cur), reward_type="dense", seed=99,
                       device=dev, global_env_offset=rank * n)
+    # overlap: "1" exchanges on the side stream (one fused call per network), "0" serialised with
+    # the paired learner step (the default), "u" serialised, one call per network
     cfg = trainer.TrainerConfig(horizon=32, seed=4, ent_coef=0.01, max_steps=40,
-                                record_cap=32 if config == "default" else 0, overlap_comm=overlap)
+                                record_cap=32 if config == "default" else 0, overlap_comm=overlap == "1",
+                                pair_learner=overlap == "0")
     tr = trainer.PGTrainer(env, cfg, process_group=group, world_size=world)
     if config == "default":
         C = pkg.CurriculumConfig
@@ -55,4 +58,4 @@ def run(out, n, iters, config, overlap=True):
 
 
 if __name__ == "__main__":
-    run(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], len(sys.argv) < 6 or sys.argv[5] == "1")
+    run(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5] if len(sys.argv) > 5 else "0")

@@ -25,15 +25,17 @@ def _port():
     return p
 
 
-def _launch(tmp, world, n, iters, config, overlap=True):
+def _launch(tmp, world, n, iters, config, mode="0"):
+    """mode: "0" the default trainer (serialised exchanges, paired learner step), "1" exchanges on
+    the side stream, "u" serialised with one learner call per network."""
     port = _port()
     procs, outs = [], []
     for r in range(world):
-        out = os.path.join(tmp, f"w{world}_r{r}_o{int(overlap)}.pt")
+        out = os.path.join(tmp, f"w{world}_r{r}_m{mode}.pt")
         env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_pg_worker.py"), out, str(n),
-                                       str(iters), config, "1" if overlap else "0"], env=env))
+                                       str(iters), config, mode], env=env))
         outs.append(out)
     for p in procs:
         assert p.wait(timeout=240) == 0
@@ -77,10 +79,11 @@ def test_overlapped_exchanges_equal_serialised(tmp_path, config):
     """Two ranks with the exchanges on the side stream (moment all-gather beside the critic's
     pass, the critic half of the gradient all-reduce beside the actor's, the scheduler codes
     beside critic values) == the same two ranks with every exchange serialised on the compute
-    stream, bit for bit: the SUMs are element-wise the same (a + b at world 2)."""
+    stream and the same per-network learner calls, bit for bit: the SUMs are element-wise the
+    same (a + b at world 2)."""
     n, iters = 256, 3
-    a = _launch(str(tmp_path), 2, n, iters, config, overlap=True)
-    b = _launch(str(tmp_path), 2, n, iters, config, overlap=False)
+    a = _launch(str(tmp_path), 2, n, iters, config, mode="1")
+    b = _launch(str(tmp_path), 2, n, iters, config, mode="u")
     for r in range(2):
         for k in ("params", "grads0", "rew0", "done0", "stats0"):
             assert torch.equal(a[r][k], b[r][k]), (r, k)

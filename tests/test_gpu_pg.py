@@ -175,13 +175,42 @@ def test_h1_recompute_is_bit_exact(pkg, n, T):
     in one workgroup (shorter than the chunk ring's look-ahead)."""
     grads = []
     for rec in (True, False):
-        _, tr = make(pkg, n, T, fused=True, h1_recompute=rec)
+        _, tr = make(pkg, n, T, fused=True, h1_recompute=rec, pair_learner=False)
         tr.rollout()
         for name in [x for x in tr.phases() if x not in ("rollout", "optimizer_step")]:
             getattr(tr, name)()
         torch.cuda.synchronize()
         grads.append(tr.grads.clone())
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("n,T,mb", [(256, 32, 1), (2048, 32, 4), (773, 64, 1)])
+def test_paired_learner_equals_two_passes(pkg, n, T, mb):
+    """dxrl_pg_fused_pair (both train passes, ONE dW2 launch for both networks, ONE reduction
+    launch) == two dxrl_pg_fused calls with the same dW2 split count, bit for bit: every
+    gradient block, the loss sums, and (PPO minibatch slices) every minibatch's gradients."""
+    outs = []
+    for paired in (True, False):
+        _, tr = make(pkg, n, T, minibatches=mb)
+        assert tr.paired
+        if not paired:
+            tr.paired = False
+            tr.splits = tr.pair_splits  # the paired step's per-network split count
+            tr.kpartial = torch.zeros(tr.splits + 16, 256, 288, device=tr.dev)
+        tr.rollout()
+        tr.critic_values()
+        tr.advantages()
+        b = tr.minibatch_bounds()
+        got = []
+        for k in range(mb):
+            tr._mb = (b[k], b[k + 1] - b[k])
+            tr.train_passes()
+            torch.cuda.synchronize()
+            got.append((tr.grads.clone(), tr.fused_loss.clone()))
+        outs.append(got)
+    for (ga, la), (gb, lb) in zip(*outs):
+        assert torch.equal(ga, gb)
+        assert torch.equal(la, lb)
 
 
 def test_adam_matches_manual(pkg):

@@ -50,9 +50,9 @@ def test_rccl_world1_collectives_and_trainer(tmp_path):
             assert torch.equal(a["params"], other["params"]), config
             if config == "default":
                 assert a["sched"] == other["sched"]
-        for suffix in ("_noupdate", "_reserve"):
+        for suffix in ("_noupdate", "_reserve", "_paired"):
             a, b = res[config + suffix]
-            assert a["overlapped"] and a["collective"]
+            assert a["collective"] and a["overlapped"] == (suffix != "_paired")
             for k in ("grads", "stats", "codes"):
                 assert len(a[k]) == len(b[k])
                 for x, y in zip(a[k], b[k]):

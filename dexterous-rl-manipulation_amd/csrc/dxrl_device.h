@@ -87,6 +87,55 @@ __device__ __forceinline__ u32x4 philox_noise(u32x4 c, uint32_t k0, uint32_t k1)
 constexpr uint32_t kStreamReset = 0x52535400u, kStreamPolicy = 0x504f4c00u, kStreamDyn = 0x44594e00u,
                    kStreamObs = 0x4f425300u;
 
+// ---------------------------------------------------------------- fused noise (config C5)
+// Block `blk` of a noise stream (kStreamDyn / kStreamObs) at counter ctr: four standard normals,
+// normal 4 blk + j in nz[j].  Throughput-mode robustness noise has distributional parity with the
+// reference's default_rng normals only (robustness_tests.py:177-207; the host-tape path replays
+// those exactly), so its generator is the build's to choose (DXRL_NOISE_GEN):
+//   0  Philox4x32-R (R = DXRL_NOISE_ROUNDS) and Box-Muller over 24-bit uniforms of (x, y), (z, w);
+//   1  (default, round 5) Philox2x32-10 (Random123: M = 0xD256D193, Weyl 0x9E3779B9) of the
+//      counter (lo ctr, hi ctr << 8 ^ stream ^ blk) under the key k0 ^ k1 * 0x9E3779B9, and
+//      Box-Muller over the 16-bit halves of each output word ((lo, hi) of word 0, then of word 1):
+//      half the 64-bit products per normal.  Config C5 rollout / C2 rollout 1.15 -> 1.12 (A/B,
+//      profiles/r05/ab_c5_noise_generators.log).
+// oracle/dx_oracle.py device_normals_f64 restates both.
+#ifndef DXRL_NOISE_GEN
+#define DXRL_NOISE_GEN 1
+#endif
+constexpr int kNoiseGen = DXRL_NOISE_GEN;
+__device__ __forceinline__ void philox2x32_10(uint32_t& c0, uint32_t& c1, uint32_t k) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p = (uint64_t)0xD256D193u * c0;  // one v_mad_u64_u32
+        const uint32_t hi = (uint32_t)(p >> 32), lo = (uint32_t)p;
+        c0 = hi ^ k ^ c1;
+        c1 = lo;
+        k += 0x9E3779B9u;
+    }
+}
+// 16-bit uniform in (0, 1]
+__device__ __forceinline__ float u01_16(uint32_t v) { return ((float)v + 1.0f) * (1.0f / 65536.0f); }
+__device__ __forceinline__ void box_muller16(uint32_t w, float& n0, float& n1) {
+    const float r = __builtin_amdgcn_sqrtf(-2.0f * __logf(u01_16(w & 0xFFFFu)));
+    float s, c;
+    __sincosf(6.28318530717958647692f * u01_16(w >> 16), &s, &c);
+    n0 = r * c;
+    n1 = r * s;
+}
+__device__ __forceinline__ void noise_normals4(uint64_t ctr, uint32_t stream, uint32_t blk, uint32_t k0, uint32_t k1,
+                                               float nz[4]) {
+    if constexpr (kNoiseGen == 1) {
+        uint32_t c0 = (uint32_t)ctr, c1 = ((uint32_t)(ctr >> 32) << 8) ^ stream ^ blk;
+        philox2x32_10(c0, c1, k0 ^ (k1 * 0x9E3779B9u));
+        box_muller16(c0, nz[0], nz[1]);
+        box_muller16(c1, nz[2], nz[3]);
+    } else {
+        const u32x4 r = philox_noise(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, blk}, k0, k1);
+        box_muller(r.x, r.y, nz[0], nz[1]);
+        box_muller(r.z, r.w, nz[2], nz[3]);
+    }
+}
+
 __device__ __forceinline__ void env_key(uint64_t seed, int64_t gid, uint32_t& k0, uint32_t& k1) {
     k0 = (uint32_t)gid ^ (uint32_t)(seed >> 32) * 0x85EBCA6Bu;
     k1 = (uint32_t)seed ^ (uint32_t)((uint64_t)gid >> 32) * 0xC2B2AE35u;
@@ -417,8 +466,12 @@ __device__ __forceinline__ void store_env(const EnvSoA& s, int64_t i, const Env&
 
 // standard normal k of Philox block k / 4 (Box-Muller pairs (x, y), (z, w)), as philox_normals
 __device__ __forceinline__ float philox_normal_at(int k, uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream) {
-    const u32x4 c = u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)(k >> 2)};
-    const u32x4 r = stream == kStreamPolicy ? philox(c, k0, k1) : philox_noise(c, k0, k1);
+    if (stream != kStreamPolicy) {  // a noise stream: its own generator (noise_normals4)
+        float nz[4];
+        noise_normals4(ctr, stream, (uint32_t)(k >> 2), k0, k1, nz);
+        return nz[k & 3];
+    }
+    const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)(k >> 2)}, k0, k1);
     float n0, n1;  // operands selected first: one branch-free Box-Muller (schedulable into MFMA gaps)
     const bool hi = (k & 2) != 0;
     box_muller(hi ? r.z : r.x, hi ? r.w : r.y, n0, n1);

@@ -39,11 +39,19 @@ template <int N>
 __device__ __forceinline__ void philox_normals(float* out, uint32_t k0, uint32_t k1, uint64_t ctr, uint32_t stream) {
 #pragma unroll
     for (int b = 0; b < (N + 3) / 4; ++b) {
-        const u32x4 c = u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)b};
-        const u32x4 r = stream == kStreamPolicy ? philox(c, k0, k1) : philox_noise(c, k0, k1);
         float n0, n1, n2, n3;
-        box_muller(r.x, r.y, n0, n1);
-        box_muller(r.z, r.w, n2, n3);
+        if (stream == kStreamPolicy) {
+            const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)b}, k0, k1);
+            box_muller(r.x, r.y, n0, n1);
+            box_muller(r.z, r.w, n2, n3);
+        } else {  // a noise stream
+            float nz[4];
+            noise_normals4(ctr, stream, (uint32_t)b, k0, k1, nz);
+            n0 = nz[0];
+            n1 = nz[1];
+            n2 = nz[2];
+            n3 = nz[3];
+        }
         if (4 * b + 0 < N) out[4 * b + 0] = n0;
         if (4 * b + 1 < N) out[4 * b + 1] = n1;
         if (4 * b + 2 < N) out[4 * b + 2] = n2;
@@ -74,11 +82,7 @@ __device__ __forceinline__ void write_policy_obs(const Env& e, bf16* xrow, float
 #pragma unroll
     for (int b = 0; b < (kObs + 3) / 4; ++b) {
         float nz[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (obs_noise > 0.0f) {
-            const u32x4 r = philox_noise(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), kStreamObs, (uint32_t)b}, k0, k1);
-            box_muller(r.x, r.y, nz[0], nz[1]);
-            box_muller(r.z, r.w, nz[2], nz[3]);
-        }
+        if (obs_noise > 0.0f) noise_normals4(ctr, kStreamObs, (uint32_t)b, k0, k1, nz);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int k = 4 * b + q;
@@ -1049,9 +1053,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     // (obs elements 4s .. 4s + 3).  Same blocks and arithmetic as philox_normal_at /
     // reset_uniform_at, so the values are identical.
     const auto normals4 = [&](uint64_t ctr, uint32_t stream, int blk, float nz[4]) {  // noise streams only
-        const u32x4 r = philox_noise(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, (uint32_t)blk}, pk0, pk1);
-        box_muller(r.x, r.y, nz[0], nz[1]);
-        box_muller(r.z, r.w, nz[2], nz[3]);
+        noise_normals4(ctr, stream, (uint32_t)blk, pk0, pk1, nz);
     };
     // Step t's action / dynamics noise and reset uniforms, computed in the head phase by the aux
     // waves, one per SIMD (waves w and w + 4 share SIMD w; Philox's 64-bit products are

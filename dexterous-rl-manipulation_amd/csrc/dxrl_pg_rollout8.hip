@@ -339,11 +339,9 @@ __global__ __launch_bounds__(kE8Threads, 1) void k_pg_rollout_e8(PgRolloutArgs p
             const bool want = is_obs ? obs_noise : (dyn && dyn_noise);
             if (!want || !env_live(e)) continue;
             const uint64_t c = is_obs ? ctr : dctr;
-            const u32x4 r = philox_noise(u32x4{(uint32_t)c, (uint32_t)(c >> 32), is_obs ? kStreamObs : kStreamDyn,
-                                               (uint32_t)b}, KEYS[e][2], KEYS[e][3]);
-            float4 nz;
-            box_muller(r.x, r.y, nz.x, nz.y);
-            box_muller(r.z, r.w, nz.z, nz.w);
+            float n4[4];
+            noise_normals4(c, is_obs ? kStreamObs : kStreamDyn, (uint32_t)b, KEYS[e][2], KEYS[e][3], n4);
+            const float4 nz = float4{n4[0], n4[1], n4[2], n4[3]};
             if (!is_obs) {
                 *reinterpret_cast<float4*>(&DR.dzn[16 * e + 4 * b]) = nz;
                 continue;

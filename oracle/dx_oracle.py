@@ -458,21 +458,63 @@ def philox4x32_10_np(c0, c1, c2, c3, k0, k1):
     return x, y, z, w
 
 
-def device_normals_f64(key, ctr, stream: int, blocks: int) -> np.ndarray:
-    """The device's Box-Muller normals (csrc/dxrl_device.h box_muller over u01_24 of one
-    Philox block: block b gives normals 4b .. 4b+3 = (r cos, r sin) of (x, y), then of (z, w)),
-    restated in f64 with libm.  The device evaluates them with hardware log / sqrt / sin / cos
-    in f32, so the values agree to ~1e-6 relative, not bit for bit: the tests use this to pin
-    WHICH draws (key, counter, stream, block) a kernel consumed.  ``ctr``: uint64 array;
-    ``key``: (k0, k1) arrays broadcastable to it.  Returns f64 [..., 4 * blocks]."""
+_P2_M, _P2_W = 0xD256D193, 0x9E3779B9
+NOISE_GEN = 1  # csrc/dxrl_device.h DXRL_NOISE_GEN: the fused-noise generator the build uses
+
+
+def philox2x32_10(ctr, key):
+    """Philox2x32-10 (Salmon et al., SC'11; Random123): 10 rounds of the 32x32->64 multiply by
+    0xD256D193 with a Weyl key bump (csrc/dxrl_device.h philox2x32_10)."""
+    x, y = (int(v) & _U32 for v in ctr)
+    k = int(key) & _U32
+    for _ in range(10):
+        p = _P2_M * x
+        x, y = ((p >> 32) ^ k ^ y) & _U32, p & _U32
+        k = (k + _P2_W) & _U32
+    return x, y
+
+
+def philox2x32_10_np(c0, c1, k):
+    """Vectorised philox2x32_10 over NumPy arrays (uint64 lanes holding u32 values)."""
+    m = np.uint64(_U32)
+    x, y = (np.asarray(v, np.uint64) & m for v in (c0, c1))
+    k = np.asarray(k, np.uint64) & m
+    for _ in range(10):
+        p = np.uint64(_P2_M) * x
+        x, y = ((p >> np.uint64(32)) ^ k ^ y) & m, p & m
+        k = (k + np.uint64(_P2_W)) & m
+    return x, y
+
+
+def device_normals_f64(key, ctr, stream: int, blocks: int, gen: int = NOISE_GEN) -> np.ndarray:
+    """The device's fused-noise normals (csrc/dxrl_device.h noise_normals4: block b gives
+    normals 4b .. 4b+3), restated in f64 with libm.  gen 1 (the build's): Philox2x32-10 of
+    (lo ctr, hi ctr << 8 ^ stream ^ b) under k0 ^ k1 * 0x9E3779B9, Box-Muller (r cos, r sin) over
+    the 16-bit halves (lo, hi) of word 0, then of word 1; gen 0: Philox4x32-10 of (lo ctr, hi ctr,
+    stream, b), Box-Muller over the 24-bit uniforms of (x, y), then (z, w).  The device evaluates
+    them with hardware log / sqrt / sin / cos in f32, so the values agree to ~1e-6 relative, not
+    bit for bit: the tests use this to pin WHICH draws (key, counter, stream, block) a kernel
+    consumed.  ``ctr``: uint64 array; ``key``: (k0, k1) arrays broadcastable to it.  Returns f64
+    [..., 4 * blocks]."""
     ctr = np.asarray(ctr, np.uint64)
+    m = np.uint64(_U32)
     out = []
     for b in range(blocks):
-        x, y, z, w = philox4x32_10_np(ctr & np.uint64(_U32), ctr >> np.uint64(32), np.full(ctr.shape, stream),
-                                      np.full(ctr.shape, b), key[0], key[1])
-        for a_, b_ in ((x, y), (z, w)):
-            ua = ((a_ >> np.uint64(8)).astype(np.float64) + 1.0) * (1.0 / 16777216.0)
-            ub = ((b_ >> np.uint64(8)).astype(np.float64) + 1.0) * (1.0 / 16777216.0)
+        if gen == 1:
+            k = (np.asarray(key[0], np.uint64) ^ ((np.asarray(key[1], np.uint64) * np.uint64(_P2_W)) & m)) & m
+            c1 = (((ctr >> np.uint64(32)) << np.uint64(8)) ^ np.uint64(stream) ^ np.uint64(b)) & m
+            w0, w1 = philox2x32_10_np(ctr & m, c1, np.broadcast_to(k, ctr.shape))
+            pairs = [((w & np.uint64(0xFFFF)), (w >> np.uint64(16))) for w in (w0, w1)]
+            scale = 1.0 / 65536.0
+            pairs = [(((lo.astype(np.float64) + 1.0) * scale), ((hi.astype(np.float64) + 1.0) * scale))
+                     for lo, hi in pairs]
+        else:
+            x, y, z, w = philox4x32_10_np(ctr & m, ctr >> np.uint64(32), np.full(ctr.shape, stream),
+                                          np.full(ctr.shape, b), key[0], key[1])
+            scale = 1.0 / 16777216.0
+            pairs = [(((a_ >> np.uint64(8)).astype(np.float64) + 1.0) * scale,
+                      ((b_ >> np.uint64(8)).astype(np.float64) + 1.0) * scale) for a_, b_ in ((x, y), (z, w))]
+        for ua, ub in pairs:
             r = np.sqrt(-2.0 * np.log(ua))
             ang = 6.283185307179586 * ub
             out += [r * np.cos(ang), r * np.sin(ang)]

@@ -138,6 +138,38 @@ def test_philox_known_answers():
         assert philox4x32_10(ctr, key) == want
 
 
+def test_philox2x32_known_answers():
+    """The oracle's Philox2x32-10 (the fused-noise generator, csrc/dxrl_device.h philox2x32_10)
+    against the Random123 known-answer vectors (kat_vectors, philox2x32 10)."""
+    from oracle.dx_oracle import philox2x32_10
+    kat = [((0, 0), 0, (0xff1dae59, 0x6cd10df2)),
+           ((0xffffffff, 0xffffffff), 0xffffffff, (0x2c3f628b, 0xab4fd7ad)),
+           ((0x243f6a88, 0x85a308d3), 0x13198a2e, (0xdd7ce038, 0xf62a4c12))]
+    for ctr, key, want in kat:
+        assert philox2x32_10(ctr, key) == want
+
+
+def test_noise_normals_restatement_gen1():
+    """device_normals_f64 (gen 1, the build's fused noise) == Philox2x32-10 of (lo ctr,
+    hi ctr << 8 ^ stream ^ block) under k0 ^ k1 * 0x9E3779B9, Box-Muller over the 16-bit halves of
+    word 0 then word 1 -- from the KAT-pinned scalar Philox."""
+    import math
+    from oracle.dx_oracle import _U32, device_normals_f64, philox2x32_10
+    ctr = np.array([0, 1, 2**40 + 5], np.uint64)
+    key = (np.array([7, 7, 9], np.uint64), np.array([11, 11, 13], np.uint64))
+    z = device_normals_f64(key, ctr, 0x4F425300, 3, gen=1)
+    for j in range(3):
+        c = int(ctr[j])
+        k = (int(key[0][j]) ^ ((int(key[1][j]) * 0x9E3779B9) & _U32)) & _U32
+        for b in range(3):
+            w = philox2x32_10((c & _U32, (((c >> 32) << 8) ^ 0x4F425300 ^ b) & _U32), k)
+            for h, word in enumerate(w):
+                ua, ub = ((word & 0xFFFF) + 1.0) / 65536.0, ((word >> 16) + 1.0) / 65536.0
+                rad = math.sqrt(-2.0 * math.log(ua))
+                assert z[j, 4 * b + 2 * h] == rad * math.cos(2 * math.pi * ub)
+                assert z[j, 4 * b + 2 * h + 1] == rad * math.sin(2 * math.pi * ub)
+
+
 def test_vectorised_philox_matches_scalar():
     """philox4x32_10_np (the full-size C5 noise checks) == the KAT-pinned scalar restatement,
     and device_normals_f64 follows the block / half / (cos, sin) order of box_muller."""
@@ -152,7 +184,7 @@ def test_vectorised_philox_matches_scalar():
         assert tuple(int(g[j]) for g in got) == want
     ctr = np.array([0, 1, 2**40 + 5], np.uint64)
     key = (np.array([7, 7, 9], np.uint64), np.array([11, 11, 13], np.uint64))
-    z = device_normals_f64(key, ctr, 0x44594E00, 2)
+    z = device_normals_f64(key, ctr, 0x44594E00, 2, gen=0)
     for j in range(3):
         for b in range(2):
             r = philox4x32_10((int(ctr[j]) & _U32, int(ctr[j]) >> 32, 0x44594E00, b), (int(key[0][j]), int(key[1][j])))

@@ -536,7 +536,9 @@ __global__ __launch_bounds__(kE8Threads, 1) void k_pg_rollout_e8(PgRolloutArgs p
         }
         if (s == 0) RW[t & 1][eg].rctr = rctr;
         // log N(a | mu, sigma) terms of the finger's action dims (gauss_logp), off the step's
-        // chain (its own basic block after the reset); the aux twin sums them next step
+        // chain (its own basic block after the reset); the aux twin sums them next step.  Forming
+        // only the first term here and the other two on the aux twin balances the two waves' P4
+        // stamps but measured no faster (profiles/r05/ab_e8_logpi_terms.log)
         __builtin_amdgcn_sched_barrier(0);
         if (finger) {
 #pragma unroll

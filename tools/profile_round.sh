@@ -29,7 +29,7 @@ if [ -z "${SKIP_PMC:-}" ]; then
   python tools/pmc_report.py "$O/pmc_fetch/**/*counter_collection.csv" "$O/pmc_write/**/*counter_collection.csv" 4194304 $O/pmc_step_kernel.json > /dev/null
   # this round's PMC file where bench.py reads roofline.traffic from (profiles/rNN/), so the bench
   # lines below cite traffic measured at the same HEAD
-  mkdir -p profiles/${ROUND:-r04} && cp $O/pmc_step_kernel.json profiles/${ROUND:-r04}/pmc_step_kernel.json
+  mkdir -p profiles/${ROUND:-r05} && cp $O/pmc_step_kernel.json profiles/${ROUND:-r05}/pmc_step_kernel.json
   step pmc_mfma 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/pmc_mfma -o run -- python3 tools/prof_pg_iter.py
   python tools/pmc_kernels.py "$O/pmc_mfma/**/*counter_collection.csv" > $O/pmc_mfma.json
   # VALU / LDS / wait view of the same iterations (8 SQ counters: one pass)
@@ -50,6 +50,12 @@ done
 if [ -z "${SKIP_EXTRA:-}" ]; then
   step bench_easy_ppo4x4 200 python bench.py --epochs 4 --minibatches 4 --steps 10 --warmup 2 --no-cpu-baseline --no-roofline
   grep '^{' $O/bench_easy_ppo4x4.log > $O/bench_easy_ppo4x4.json
+  step prof_easy_ppo4x4 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_easy_ppo4x4 -o run -- \
+    python3 bench.py --epochs 4 --minibatches 4 --steps 10 --warmup 2 --no-cpu-baseline --no-roofline
+  grep '^{' $O/prof_easy_ppo4x4.log > $O/prof_easy_ppo4x4.json
+  # the cold-start C2 line: no clock prewarm before the warmup iterations
+  step bench_easy_cold 200 python bench.py --prewarm-s 0 --no-cpu-baseline --no-roofline
+  grep '^{' $O/bench_easy_cold.log > $O/bench_easy_cold.json
   step bench_default_restart 200 python bench.py --config default --sched-restart --no-cpu-baseline --no-roofline
   grep '^{' $O/bench_default_restart.log > $O/bench_default_restart.json
   step bench_default_training 200 python bench.py --config default --success-rule training --no-cpu-baseline --no-roofline
@@ -59,8 +65,20 @@ if [ -z "${SKIP_EXTRA:-}" ]; then
   step eval_bench 200 python tools/eval_bench.py
   grep '^{' $O/eval_bench.log > $O/eval_bench.jsonl
 fi
+# interleaved rollout A/B on one box (DESIGN §9 ratios): C2 easy (16-env kernel) and C5 variable +
+# noise at 4096 envs, C4 hard at 8192 envs (32-env kernel; ws16 = the 16-env kernel forced)
+if [ -z "${SKIP_RT:-}" ]; then
+  for i in 1 2 3; do
+    step rt_easy_$i 120 env CUR=easy DIAGS=0:ws python tools/rollout_time.py
+    step rt_variable_$i 120 env CUR=variable DIAGS=0:ws python tools/rollout_time.py
+    step rt_hard8192_$i 120 env CUR=hard ENVS=8192 DIAGS=0:e8,2048:ws16 python tools/rollout_time.py
+  done
+  grep -h -v amdgpu $O/rt_*.log > $O/rollout_ratio_ab.log
+  step stamps_ws 120 python tools/rollout_stamps.py
+  step stamps_e8 120 env ENVS=8192 python tools/rollout_stamps.py
+fi
 if [ -z "${SKIP_SWEEP:-}" ]; then step step_sweep 300 python tools/step_sweep.py 12 24; grep '^{' $O/step_sweep.log > $O/step_sweep.jsonl; fi
-for c in $CFGS; do
+for c in $CFGS easy_ppo4x4; do
   f=$(ls $O/prof_$c/*kernel_trace.csv $O/prof_$c/*/*kernel_trace.csv 2>/dev/null | head -1)
   [ -n "$f" ] && python tools/trace_summary.py "$f" > $O/trace_summary_$c.txt
 done

@@ -205,7 +205,7 @@ __device__ __forceinline__ void wave_layer(const bf16* A, int lda, const WF& wfr
 // live rows in a 32-row MFMA: twice the matrix-core cycles per output).  A chain of 16x16x32
 // MFMAs over k-steps of 32 rounds exactly like the 32x32x16 chain over the same k order
 // (tools/mfma_order.hip: 0 of 131,072 outputs differ), so the hidden units stay bit-identical to
-// the learner's forward and to k_pg_rollout_ls.  Transposed formulation (weights as the A
+// the learner's forward and to the one-lane k_pg_rollout.  Transposed formulation (weights as the A
 // operand, as in the learner): lane l's accumulator holds columns n0 + 16 j + 4 (l >> 4) .. +3 of
 // activation row l & 15, so the tanh epilogue runs on packed pairs and leaves as one 8-byte LDS
 // store per tile.  Fragments: A row l & 15, k 32 k + 8 (l >> 4) ..+7; wfrag(j, k) =
@@ -426,426 +426,18 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout(PgRolloutA
     }
 }
 
-// ------------------------------------------------------------------ lane-split rollout
-// k_pg_rollout_ls: the same rollout as k_pg_rollout (same Philox streams and counters, the
-// same arithmetic, so the two kernels write bit-identical tapes), re-laid-out for latency.
-// A workgroup owns 16 envs (4096 envs -> 256 workgroups, one per CU) and each env is spread
-// over 16 lanes of one wave: lane s owns joint s (jp, jv), lanes 0..2 the object's axis s,
-// and every lane keeps a copy of the env's scalars (flags, step, size, mass, friction ...).
-// Elementwise physics runs lane-parallel; the reference's ordered sums (finger sums, the
-// closure term, log pi) are gathered through a per-env LDS row and added in the reference order
-// on every lane.  The actor MLP runs on all four waves as in k_pg_rollout, on one 32-row
-// MFMA tile of which rows 0..15 are this workgroup's envs.
-constexpr int kLsEnvs = 16;  // 16 lanes per env: envs per workgroup = 256 threads / 16
-
-// In-group exchange through a per-env LDS row (dwords): one LDS write + wide reads replace a
-// chain of ds_bpermute shuffles.  All 16 lanes of a group are in one wave, so a wavefront-scope
-// fence (compiler ordering + lgkmcnt) is the only synchronisation needed.
-constexpr int kGx = 72, kGxJp = 0, kGxTerm = 16, kGxNacc = 32, kGxD = 40, kGxOp = 50, kGxV2 = 56;
-__device__ __forceinline__ void wsync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
-// Lane-split contacts_of: every lane of the group gets the mask and the minimum distance.
-// gbit: this group's bit offset in the wave's ballot; op: the object position (all lanes).
-__device__ __forceinline__ uint32_t ls_contacts(float jp, const double op[3], double size, int s, int gbit,
-                                                double& dmin, float g3[3], float* gx) {
-    gx[kGxJp + s] = jp;
-    wsync();
-    const int f = s < kF ? s : 0;
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) g3[j] = gx[kGxJp + kJ * f + j];
-    float sum = g3[0];
-#pragma unroll
-    for (int j = 1; j < kJ; ++j) sum = sum + g3[j];
-    const double tip = (double)(sum * kC01);
-    const double dx = tip - op[0], dy = tip - op[1], dz = tip - op[2];
-    const double d = sqrt((dx * dx + dy * dy) + dz * dz);
-    const bool hit = s < kF && d < size * 1.5;
-    const uint32_t mask = (uint32_t)(__ballot(hit) >> gbit) & ((1u << kF) - 1u);
-    double* gd = reinterpret_cast<double*>(gx + kGxD);
-    if (s < kF) gd[s] = d;
-    wsync();
-    dmin = gd[0];
-#pragma unroll
-    for (int k = 1; k < kF; ++k) {
-        const double dk = gd[k];
-        dmin = dk < dmin ? dk : dmin;
-    }
-    return mask;
-}
-
-// the object position from lanes 0..2 to every lane of the group
-__device__ __forceinline__ void ls_object(double opd, int s, double op[3], float* gx) {
-    double* go = reinterpret_cast<double*>(gx + kGxOp);
-    if (s < 3) go[s] = opd;
-    wsync();
-#pragma unroll
-    for (int d = 0; d < 3; ++d) op[d] = go[d];
-}
-
-__global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRolloutArgs p) {
-    constexpr int kRows = 32;  // MFMA row tile; rows >= kLsEnvs are padding
-    __shared__ __attribute__((aligned(16))) bf16 W1s[kH * kW1s];
-    __shared__ __attribute__((aligned(16))) bf16 W3s[kOut * kW3s];
-    __shared__ __attribute__((aligned(16))) bf16 X[kRows * kXs];
-    __shared__ __attribute__((aligned(16))) bf16 H1[kRows * kHs];
-    __shared__ __attribute__((aligned(16))) bf16 H2[kRows * kHs];
-    __shared__ float MU[kLsEnvs * (kOut + 1)];
-    __shared__ float LS[kActPad], SIG[kActPad], ISIG[kActPad];
-    __shared__ __attribute__((aligned(16))) float GX[kLsEnvs * kGx];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int eg = tid >> 4, s = tid & 15, gbit = 16 * (eg & 3);
-    float* gx = GX + eg * kGx;
-    const int64_t n = p.s.n;
-    const int64_t i = (int64_t)blockIdx.x * kLsEnvs + eg;
-    const bool live = i < n;
-    const int64_t T = p.horizon;
-    if (tid < kAct) {
-        const float ls = p.params[kOffLogStd + tid];
-        LS[tid] = ls;
-        SIG[tid] = __expf(ls);
-        ISIG[tid] = __expf(-ls);
-    }
-    WTile<kH / 16> w2[kNT];
-#pragma unroll
-    for (int j = 0; j < kNT; ++j) load_wtile(w2[j], p.wbf + kBfW2a, kHx, kCpw * wave + 32 * j, lane);
-    WTile<kH / 16> w3r;  // the mu wave's W3 fragments (rows = head outputs)
-    if (wave == kRolloutWaves - 1) load_wtile(w3r, p.wbf + kBfW3a, kHx, 0, lane);
-    for (int c = tid; c < kH * (kIn / 8); c += 64 * kRolloutWaves) {
-        const int row = c / (kIn / 8), col = 8 * (c % (kIn / 8));
-        *reinterpret_cast<bf16x8*>(W1s + row * kW1s + col) =
-            *reinterpret_cast<const bf16x8*>(p.wbf + kBfW1a + (int64_t)row * kIn + col);
-    }
-    for (int c = tid; c < kOut * (kH / 8); c += 64 * kRolloutWaves) {
-        const int row = c / (kH / 8), col = 8 * (c % (kH / 8));
-        *reinterpret_cast<bf16x8*>(W3s + row * kW3s + col) =
-            *reinterpret_cast<const bf16x8*>(p.wbf + kBfW3a + (int64_t)row * kHx + col);
-    }
-    // padding rows and the constant columns of the X tile (bias column 45 = 1)
-    for (int c = tid; c < kRows * kXs; c += 64 * kRolloutWaves) {
-        const int row = c / kXs, col = c % kXs;
-        X[c] = (row < kLsEnvs && col == kObsIn) ? (bf16)1.0f : (bf16)0.0f;
-    }
-    for (int c = tid; c < (kRows - kLsEnvs) * kHs; c += 64 * kRolloutWaves) {
-        H1[kLsEnvs * kHs + c] = (bf16)0.0f;
-        H2[kLsEnvs * kHs + c] = (bf16)0.0f;
-    }
-    const int r32 = lane & 31, h2 = lane >> 5;
-    const auto w1frag = [&](int j, int k) {
-        return *reinterpret_cast<const bf16x8*>(W1s + (kCpw * wave + 32 * j + r32) * kW1s + 16 * k + 8 * h2);
-    };
-    const auto w2frag = [&](int j, int k) { return w2[j].b[k]; };
-
-    // ---- per-lane env state
-    float jp = 0.0f, jv = 0.0f;  // joint s
-    double opd = 0.0;            // object axis s (s < 3)
-    float ovd = 0.0f;
-    uint32_t flags = 0;
-    int32_t et = 0, cfg = 0;
-    double size = 0.0, mass = 0.0, fric = 0.0, ep_ret = 0.0, sum_ret = 0.0;
-    int32_t cnt = 0, sum_len = 0, succ = 0;
-    uint64_t rctr = 0;
-    uint32_t ek0 = 0, ek1 = 0, pk0 = 0, pk1 = 0;
-    if (live) {
-        if (s < kD) {
-            jp = p.s.jp[(int64_t)s * n + i];
-            jv = p.s.jv[(int64_t)s * n + i];
-        }
-        if (s < 3) {
-            opd = p.s.op[(int64_t)s * n + i];
-            ovd = p.s.ov[(int64_t)s * n + i];
-        }
-        flags = p.s.flags[i];
-        et = p.s.t[i];
-        size = p.s.size[i];
-        mass = p.s.mass[i];
-        fric = p.s.fric[i];
-        cfg = p.s.cfg[i];
-        ep_ret = p.ep_ret[i];
-        rctr = p.s.reset_ctr[i];
-        env_key(p.env_seed, p.gid0 + i, ek0, ek1);
-        env_key(p.policy_seed, p.gid0 + i, pk0, pk1);
-    }
-    // this lane's reset slot 15 + s2 of the env's curriculum row (the row is fixed for the launch)
-    const int s2 = s < DXRL_RESET_EXTRA ? s : 0;
-    double lo2 = 0.0, hi2 = 0.0, cst2 = 0.0;
-    bool has2 = true, fric64 = false;
-    if (live) {
-        const dxrl_curriculum& cu = p.s.curricula[cfg];
-        const double* rg = s2 == 0 ? cu.size_range
-                                   : s2 == 1 ? cu.mass_range
-                                             : s2 == 2 ? cu.friction_range
-                                                       : s2 == 3 ? cu.spawn_x_range : s2 == 4 ? cu.spawn_y_range : cu.spawn_z_range;
-        lo2 = rg[0];
-        hi2 = rg[1];
-        cst2 = s2 == 0 ? cu.object_size : s2 == 1 ? cu.object_mass : cu.friction_coefficient;
-        has2 = s2 == 0 ? cu.has_size_range != 0 : s2 == 1 ? cu.has_mass_range != 0 : s2 == 2 ? cu.has_friction_range != 0 : true;
-        fric64 = cu.friction_is_f64_scalar != 0;
-    }
-    // observation row of this env (+ observation noise): lane s writes jp[s], jv[s], the
-    // object axis s, a quaternion slot and a contact bit -- element k of ME:254-264
-    const auto write_obs_row = [&](uint64_t ctr) {
-        bf16* xr = X + eg * kXs;
-        const auto put = [&](int k, float v) {
-            if (p.obs_noise > 0.0f) v = v + p.obs_noise * philox_normal_at(k, pk0, pk1, ctr, kStreamObs);
-            xr[k] = to_bf16(v);
-        };
-        if (s < kD) {
-            put(s, jp);
-            put(kD + s, jv);
-        }
-        if (s < 3) {
-            put(2 * kD + s, (float)opd);
-            put(2 * kD + 7 + s, ovd);
-        } else if (s < 7) {
-            put(2 * kD + s, s == 3 ? 1.0f : 0.0f);  // identity quaternion (ME:164)
-        } else if (s < 7 + kF) {
-            put(2 * kD + 10 + (s - 7), (float)((flags >> (s - 7)) & 1u));
-        }
-    };
-    const auto tape_obs_row = [&](int64_t m) {  // 64 bf16 = 16 lanes x 8 bytes
-        *reinterpret_cast<bf16x4*>(p.obs_rm + m * kIn + 4 * s) = *reinterpret_cast<const bf16x4*>(X + eg * kXs + 4 * s);
-    };
-    const bool mlp = !(p.diag & 1);
-    unsigned long long st_acc[8], st_last = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) st_acc[k] = 0;
-#define LS_STAMP(k)                                                                              \
-    do {                                                                                         \
-        if (p.diag & 32) {                                                                       \
-            __builtin_amdgcn_sched_barrier(0);                                                   \
-            unsigned long long t_;                                                               \
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
-            __builtin_amdgcn_sched_barrier(0);                                                   \
-            st_acc[k] += t_ - st_last;                                                           \
-            st_last = t_;                                                                        \
-        }                                                                                        \
-    } while (0)
-    LS_STAMP(7);
-    for (int64_t t = 0; t < T; ++t) {
-        const int64_t m = t * n + i;
-        const uint64_t ctr = p.iteration * (uint64_t)T + (uint64_t)t;
-        if (live) write_obs_row(ctr);
-        LS_STAMP(0);
-        __syncthreads();
-        if (live) tape_obs_row(m);
-        if (mlp) wave_layer<kIn / 16, kNT, true, 1>(X, kXs, w1frag, kCpw * wave, nullptr, 0, H1, kHs, lane);
-        __syncthreads();
-        LS_STAMP(1);
-        // This step's Philox draws (action noise, dynamics noise, the next reset's two uniforms)
-        // depend only on counters, so they are issued in the L2 block, where the scheduler can
-        // place them in the gaps of the MFMA chain instead of on the step's serial path.
-        const int sa = s < kAct ? s : 0;
-        float eps = 0.0f, dzn = 0.0f;
-        double u1 = 0.0, u2 = 0.0;
-        const auto draws = [&]() {
-            eps = philox_normal_at(sa, pk0, pk1, ctr, kStreamPolicy);
-            if (p.dyn_noise > 0.0f) dzn = philox_normal_at(sa, pk0, pk1, ctr, kStreamDyn);
-            u1 = reset_uniform_at(s < kD ? s : 0, ek0, ek1, rctr);
-            u2 = reset_uniform_at(kD + s2, ek0, ek1, rctr);
-        };
-        if (mlp) {
-            draws();
-            wave_layer<kH / 16, kNT, true, 1>(H1, kHs, w2frag, kCpw * wave, p.params + kOffW2a + kH, kHx, H2, kHs,
-                                              lane);
-        } else {
-            draws();
-        }
-        __syncthreads();
-        LS_STAMP(2);
-        if (mlp && wave == kRolloutWaves - 1) {  // mu head: 16 env rows x 32 head rows
-            f32x16 acc;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-            bf16x8 ah[kH / 16];
-#pragma unroll
-            for (int k = 0; k < kH / 16; ++k) ah[k] = *reinterpret_cast<const bf16x8*>(H2 + r32 * kHs + 16 * k + 8 * h2);
-#pragma unroll
-            for (int k = 0; k < kH / 16; ++k) acc = mfma32(ah[k], w3r.b[k], acc);
-            const float bias = p.params[kOffW3a + (int64_t)r32 * kHx + kH];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) MU[acc_row(q, lane) * (kOut + 1) + r32] = acc[q] + bias;  // rows < 16
-        }
-        __syncthreads();
-        LS_STAMP(3);
-        if (!live) continue;
-        // ---- a = mu + sigma * eps, log pi(a|s) in action order (gauss_logp's order)
-        const float mu = mlp ? MU[eg * (kOut + 1) + sa] : 0.0f;
-        float a = mu + SIG[sa] * eps;
-        const float z = (a - mu) * ISIG[sa];
-        const float term = -0.5f * z * z - LS[sa] - 0.5f * kLog2Pi;
-        gx[kGxTerm + s] = term;
-        wsync();
-        float lp = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 t4 = reinterpret_cast<const float4*>(gx + kGxTerm)[q];
-            lp += t4.x;
-            lp += t4.y;
-            lp += t4.z;
-            if (4 * q + 3 < kAct) lp += t4.w;
-        }
-        p.act[m * kActPad + s] = s < kAct ? a : 0.0f;
-        if (s == 0) p.logp[m] = lp;
-        if (p.dyn_noise > 0.0f)  // robustness_tests.py:180-187 (the tape keeps the policy's action)
-            a = clipf(a + p.dyn_noise * dzn, -1.0f, 1.0f);
-        if (p.applied_act) p.applied_act[m * kActPad + s] = s < kAct ? a : 0.0f;
-        LS_STAMP(4);
-        bool te = false, tr = false;
-        double r = 0.0;
-        if (!(p.diag & 2)) {
-            // ---- env_step, lane-split (ME:198-252)
-            if (s < kD) {
-                const float ak = clipf(a, -1.0f, 1.0f);
-                jv = kC09 * jv + kC01 * ak;
-                jp = clipf(jp + jv * kDt, -1.0f, 1.0f);
-            }
-            {
-                const double damp = 1.0 - (fric * 0.1 * 0.01);
-                const float dampf = (float)damp;
-                const bool op32 = (flags & kOpIsF32) != 0, fric_f64 = (flags & kFricF64) != 0;
-                const int ax = s < 3 ? s : 0;
-                const double gz = ax == 2 ? kGz : 0.0, lo = ax == 2 ? 0.0 : -0.2, hi = ax == 2 ? 0.3 : 0.2;
-                float v = fric_f64 ? (float)((double)ovd * damp) : ovd * dampf;
-                v = (float)((double)v + gz);
-                const float inc = v * kDt;
-                double q = op32 ? (double)((float)opd + inc) : opd + (double)inc;
-                q = clipd(q, lo, hi);
-                if ((q <= lo && v < 0.0f) || (q >= hi && v > 0.0f)) v = 0.0f;
-                if (s < 3) {
-                    opd = q;
-                    ovd = v;
-                }
-            }
-            flags &= ~kOpIsF32;
-            double op3[3];
-            ls_object(opd, s, op3, gx);
-            double dmin;
-            float g3[3];
-            const uint32_t c = ls_contacts(jp, op3, size, s, gbit, dmin, g3, gx);
-            // dense_reward (RS:101-187)
-            const double dist = exp(-5.0 * dmin);
-            const double con = count_over_f_f64(__popc(c));
-            float nacc = 0.0f;  // finger s: sum of its negative joint positions
-#pragma unroll
-            for (int j = 0; j < kJ; ++j)
-                if (g3[j] < 0.0f) nacc = nacc + g3[j];
-            if (s < kF) gx[kGxNacc + s] = nacc;
-            wsync();
-            float sum = 0.0f;
-#pragma unroll
-            for (int f = 0; f < kF; ++f) sum = sum + (-gx[kGxNacc + f]);
-            const float avg = div_f(sum);
-            const float clo = clipf(div_f(avg), 0.0f, 1.0f);
-            float st = 0.0f;
-            if (flags & kHasPrev) {
-                const uint32_t prev = (flags >> kPrevShift) & 0xFFu;
-                float ch = 0.0f;
-#pragma unroll
-                for (int f = 0; f < kF; ++f) ch = ch + (float)(((c ^ prev) >> f) & 1u);
-                st = clipf(1.0f - count_over_f_f32((uint32_t)ch), 0.0f, 1.0f);
-            }
-            flags = (flags & ~(0xFFu << kPrevShift)) | (c << kPrevShift) | kHasPrev;
-            r = ((p.w.w_dist * dist + p.w.w_con * con) + p.w.w_clo * (double)clo) + p.w.w_st * (double)st;
-            flags = (flags & ~0xFFu) | c;
-            te = __popc(c) >= 3;
-            tr = et >= p.max_episode_steps;
-            et += 1;
-        }
-        LS_STAMP(5);
-        ep_ret += r;
-        const bool d = !(p.diag & 2) && (te || tr || et >= p.max_steps);
-        if (s == 0) {
-            p.rew[m] = (float)r;
-            p.done[m] = d;
-            if (p.ep_code)
-                p.ep_code[m] = d ? (uint16_t)((et << 1) | (p.success_terminated && te ? 1 : 0)) : (uint16_t)0;
-        }
-        if (d) {
-            if (s == 0 && cnt < p.record_cap) {
-                const int64_t o = i * p.record_cap + cnt;
-                p.rec_return[o] = ep_ret;
-                p.rec_length[o] = et;
-                p.rec_success[o] = p.success_terminated ? (uint8_t)te : (uint8_t)0;
-                p.rec_end_step[o] = (int32_t)t;
-            }
-            ++cnt;
-            sum_ret += ep_ret;
-            sum_len += et;
-            succ += te;
-            // ---- env_reset_philox, lane-split: lane s draws slot s (joint) and slot 15 + s
-            const double v2 = has2 ? lo2 + (hi2 - lo2) * u2 : cst2;  // config.py:44-113 samplers
-            if (s < kD) {
-                jp = (float)(-0.1 + (0.1 - -0.1) * u1);
-                jv = 0.0f;
-            }
-            double* gv = reinterpret_cast<double*>(gx + kGxV2);
-            if (s < DXRL_RESET_EXTRA) gv[s] = v2;
-            wsync();
-            size = gv[0];
-            mass = gv[1];
-            fric = gv[2];
-            const double spawn = gv[3 + (s < 3 ? s : 0)];
-            const bool has = (flags & kHasObject) != 0;
-            if (s < 3) {
-                opd = (double)(float)(has ? opd : spawn);
-                ovd = 0.0f;
-            }
-            et = 0;
-            flags = kOpIsF32 | kHasObject | (fric64 ? kFricF64 : 0u);
-            double op3[3];
-            ls_object(opd, s, op3, gx);
-            double dmin;
-            float g3[3];
-            flags |= ls_contacts(jp, op3, size, s, gbit, dmin, g3, gx);
-            ++rctr;
-            ep_ret = 0.0;
-        }
-        LS_STAMP(6);
-    }
-    if ((p.diag & 32) && s == 0 && live) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) p.stamps[i * 8 + k] = st_acc[k];
-    }
-#undef LS_STAMP
-    if (live) {
-        // bootstrap observation (slot T), then the state back to the slab
-        write_obs_row(p.iteration * (uint64_t)T + (uint64_t)T);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        tape_obs_row(T * n + i);
-        if (s < kD) {
-            p.s.jp[(int64_t)s * n + i] = jp;
-            p.s.jv[(int64_t)s * n + i] = jv;
-        }
-        if (s < 3) {
-            p.s.op[(int64_t)s * n + i] = opd;
-            p.s.ov[(int64_t)s * n + i] = ovd;
-        }
-        if (s == 0) {
-            p.s.flags[i] = flags;
-            p.s.t[i] = et;
-            p.s.size[i] = size;
-            p.s.mass[i] = mass;
-            p.s.fric[i] = fric;
-            p.s.reset_ctr[i] = rctr;
-            p.ep_ret[i] = ep_ret;
-            p.ep_count[i] = cnt;
-            p.ep_sum_ret[i] = sum_ret;
-            p.ep_sum_len[i] = sum_len;
-            p.ep_succ[i] = succ;
-        }
-    }
-}
+// 16 lanes per env (k_pg_rollout_ws): envs per 256 env lanes.  (Round 5 retired the 4-wave
+// lane-split kernel k_pg_rollout_ls, diag 64: k_pg_rollout_ws is its 8-wave successor and the
+// one-lane k_pg_rollout and 32-env k_pg_rollout_e8 remain its bit-identity twins.)
+constexpr int kLsEnvs = 16;
 
 // ------------------------------------------------------------------ warp-specialised rollout
-// k_pg_rollout_ws: the lane-split rollout with the work that does not depend on this step's
-// env state taken off the env lanes' serial chain.  A workgroup owns 16 envs as in
-// k_pg_rollout_ls, with 8 waves (two per SIMD):
-//   * env waves 0..3: lane (env 4w + row, s) exactly as k_pg_rollout_ls -- observation row,
-//     sampling, dynamics, contacts, termination, auto-reset;
+// k_pg_rollout_ws: the lane-split rollout -- each env spread over the 16 lanes of one DPP row
+// (lane s owns joint s, lanes 0..2 the object's axis s, every lane a copy of the env's scalars)
+// -- with the work that does not depend on this step's env state taken off the env lanes'
+// serial chain.  A workgroup owns 16 envs with 8 waves (two per SIMD):
+//   * env waves 0..3: lane (env 4w + row, s) -- observation row, sampling, dynamics, contacts,
+//     termination, auto-reset;
 //   * aux waves 4..7: wave 4 + w is the lane-for-lane twin of env wave w.  While the env lanes
 //     step, the twin computes log pi and the act / log pi tape and settles the PREVIOUS step's
 //     dense reward and episode bookkeeping (return, records, sums) from the inputs the env lanes
@@ -854,7 +446,7 @@ __global__ __launch_bounds__(64 * kRolloutWaves, 1) void k_pg_rollout_ls(PgRollo
 //     16 envs (step_draws) while the env waves run the action-independent object update;
 //   * all 8 waves split the actor MLP: one 32-column tile of L1 and of L2 each (two waves per
 //     SIMD, so one wave's tanh epilogue overlaps the other's MFMAs); aux wave 7 runs the mu head.
-// Every value is computed by the same instruction sequence as in k_pg_rollout_ls (same MFMA
+// Every value is computed by the same instruction sequence as in k_pg_rollout (same MFMA
 // tiles and K order, same Philox calls, same reward ops), so the tapes are bit-identical.
 // Exchanges inside an env's 16 lanes are DPP row broadcasts (an env is one DPP row).
 constexpr int kWsWaves = 8, kWsThreads = 64 * kWsWaves;
@@ -1046,7 +638,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     }
 
     // ---- aux: Philox draws.  Each block is computed once per env row and its values written
-    // straight into the LDS slots of the env lanes that use them (k_pg_rollout_ls recomputes the
+    // straight into the LDS slots of the env lanes that use them (a lane-split kernel that draws on
     // shared blocks on every lane): lanes 0..10 reset block s (slots 2s, 2s + 1: joint slots 0..14
     // -> u1 of lane k, extra slots 15..20 -> u2 of lane k - 15); lanes 11..14 action- and
     // dynamics-noise block s - 11 (normals 4(s-11) .. +3); lanes 0..11 observation-noise block s
@@ -2059,8 +1651,8 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                     a->applied_act,
                     a->dyn_noise_tape,
                     a->obs_noise_tape};
-    DXRL_REQUIRE(!(a->dyn_noise_tape || a->obs_noise_tape) || !(a->obs_fm || (a->diag_flags & (16 | 32 | 64))),
-                 "the noise tapes are written by the default (warp-specialised) rollout kernel only");
+    DXRL_REQUIRE(!(a->dyn_noise_tape || a->obs_noise_tape) || !(a->obs_fm || (a->diag_flags & 16)),
+                 "the noise tapes are written by the 16- and 32-env rollout kernels only");
     DeviceGuard g(env->device);
     const int64_t n = env->cfg.num_envs;
     if (a->obs_fm || (a->diag_flags & 16)) {  // feature-major tape / A-B reference: the 64-env kernel
@@ -2068,9 +1660,10 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                            as_stream(stream), p);
         return launch_check("k_pg_rollout");
     }
+    DXRL_REQUIRE(!(a->diag_flags & (32 | 64)), "diag_flags 32 / 64 named the retired k_pg_rollout_ls");
     static unsigned long long* stamps = nullptr;
     static int64_t stamps_n = 0;
-    if ((a->diag_flags & (32 | 128)) && stamps_n < n) {
+    if ((a->diag_flags & 128) && stamps_n < n) {
         if (stamps) (void)hipFree(stamps);
         (void)hipMalloc(&stamps, (size_t)n * 16 * sizeof(unsigned long long));
         stamps_n = n;
@@ -2083,14 +1676,14 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
     }();
     // >= 32 envs per CU: the 32-env kernel runs them in one round (the 16-env kernel would need
     // two); diag 1024 / 2048 force the 32-env / 16-env kernel (A/B, bit-identity tests)
-    const bool e8 = !(a->diag_flags & (32 | 64 | 2048)) && ((a->diag_flags & 1024) || n >= (int64_t)kE8Envs * cus);
+    const bool e8 = !(a->diag_flags & 2048) && ((a->diag_flags & 1024) || n >= (int64_t)kE8Envs * cus);
     if (e8) {
         const bool noise = a->obs_noise_std > 0.0 || a->dyn_noise_std > 0.0 || a->dyn_noise_tape || a->obs_noise_tape;
         const bool diag = (a->diag_flags & ~(1024 | 2048)) != 0 || a->applied_act || a->dyn_noise_tape ||
                           a->obs_noise_tape;
         return launch_pg_rollout_e8(p, n, noise, diag, as_stream(stream));
     }
-    if (!(a->diag_flags & (32 | 64))) {  // default: the warp-specialised kernel
+    {  // the 16-env warp-specialised kernel
         const bool noise = a->obs_noise_std > 0.0 || a->dyn_noise_std > 0.0 || a->dyn_noise_tape || a->obs_noise_tape;
         const bool diag = (a->diag_flags & ~(1024 | 2048)) != 0 || a->applied_act || a->dyn_noise_tape ||
                           a->obs_noise_tape;
@@ -2130,22 +1723,6 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
         }
         return DXRL_OK;
     }
-    hipLaunchKernelGGL(k_pg_rollout_ls, dim3((unsigned)((n + kLsEnvs - 1) / kLsEnvs)), dim3(64 * kRolloutWaves), 0,
-                       as_stream(stream), p);
-    if (int rc = launch_check("k_pg_rollout_ls")) return rc;
-    if (a->diag_flags & 32) {  // diagnostic builds: mean cycles per env per step segment
-        std::vector<unsigned long long> h((size_t)n * 8);
-        (void)hipStreamSynchronize(as_stream(stream));
-        (void)hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost);
-        fprintf(stderr, "rollout_ls cycles/step:");
-        for (int k = 0; k < 8; ++k) {
-            double sum = 0;
-            for (int64_t e = 0; e < n; ++e) sum += (double)h[e * 8 + k];
-            fprintf(stderr, " s%d=%.0f", k, sum / n / a->horizon);
-        }
-        fprintf(stderr, "\n");
-    }
-    return DXRL_OK;
 }
 
 int dxrl_pg_gae_partial_doubles(int64_t num_envs, int64_t horizon, int64_t* doubles) {

@@ -42,7 +42,7 @@ struct PgRolloutArgs {
     float* applied_act;  // [T N][kActPad] the action the env integrated (nullable; parity checks)
     float* dyn_noise_tape;  // [T N][kActPad] f32(sigma) * z as added to the action (nullable; ws kernel)
     float* obs_noise_tape;  // [(T+1) N][kObsNoiseLd] f32(sigma) * z per observation element (nullable)
-    unsigned long long* stamps;  // diag & 32 (k_pg_rollout_ls): cycles per step segment
+    unsigned long long* stamps;  // diag & 128: cycles per step segment (16- / 32-env kernels)
 };
 constexpr int kObsNoiseLd = 48;
 

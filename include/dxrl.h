@@ -272,12 +272,13 @@ typedef struct dxrl_pg_rollout_args {
     int32_t* ep_sum_length;    /* i32 [N]                                                  */
     int32_t* ep_successes;     /* i32 [N] finished episodes that terminated (>= 3 contacts) */
     int32_t diag_flags;        /* diagnostics only (timing ablations): bit0 skip the actor MLP
-                                  (mu = 0), bit1 skip the env step; kernel selection: 16 the
-                                  one-lane-per-env kernel, 64 the 4-wave lane-split kernel
-                                  (bit-identical tapes); 32 / 128 per-step cycle stamps of the
-                                  lane-split / warp-specialised kernel (printed to stderr);
-                                  256 skip the warp-specialised kernel's draws, 512 its reward
-                                  settle (timing only: results are wrong); 0 in every real run */
+                                  (mu = 0), bit1 skip the env step; kernel selection (bit-
+                                  identical tapes): 16 the one-lane-per-env kernel, 1024 the
+                                  32-env kernel (default at >= 32 envs per CU), 2048 the 16-env
+                                  kernel at any size; 128 per-step cycle stamps of the 16- / 32-env
+                                  kernel (printed to stderr); 256 skip the 16-env kernel's draws,
+                                  512 its reward settle (timing only: results are wrong); 32 / 64
+                                  (the retired 4-wave kernel) are rejected; 0 in every real run */
     int32_t success_rule;      /* DXRL_SUCCESS_* for the episode records                   */
     int32_t record_cap;        /* per-env episode records [N][record_cap] (0 = none)       */
     double* rec_return;

@@ -333,13 +333,13 @@ def test_fused_dynamics_noise(pkg, std):
                                          ("variable", 4100, 0.05)])
 def test_lane_split_rollout_matches_64_env_kernel(pkg, cur, n, noise):
     """k_pg_rollout_ws (default: 16 envs x 16 lanes, env waves + aux twin waves, 8 waves),
-    k_pg_rollout_ls (diag 64: the same lanes on 4 waves), k_pg_rollout (diag 16: one lane
-    per env) and k_pg_rollout_e8 (diag 1024: 32 envs x 8 lanes, the kernel of >= 32 envs per CU)
-    share every Philox stream and every op: tapes, episode records and env state are equal bit
-    for bit (auto-resets, observation / dynamics noise, a ragged last workgroup)."""
+    k_pg_rollout (diag 16: one lane per env) and k_pg_rollout_e8 (diag 1024: 32 envs x 8 lanes,
+    the kernel of >= 32 envs per CU) share every Philox stream and every op: tapes, episode
+    records and env state are equal bit for bit (auto-resets, observation / dynamics noise, a
+    ragged last workgroup)."""
     T = 24
     outs = []
-    for diag in (16, 64, 0, 1024):
+    for diag in (16, 0, 1024):
         env = pkg.envs.VecEnv(n, curriculum_config=pkg.CurriculumConfig.named(cur), reward_type="dense", seed=11)
         cfg = pkg.trainer.TrainerConfig(horizon=T, seed=5, max_steps=13, record_cap=T, obs_noise_std=noise,
                                         dyn_noise_std=noise)

@@ -1,6 +1,6 @@
 """Per-step segment cycles of the PG rollout (diagnostic only): DIAG=128 -> k_pg_rollout_ws
 stamps (s0 obs row, s1 L1, s2 L2, s3 head phase, s4 head barrier wait, s5 P4, s6 P4 barrier),
-DIAG=32 -> k_pg_rollout_ls; at ENVS >= 32 per CU (or DIAG | 1024) the 32-env k_pg_rollout_e8.  Configs: easy, hard, easy + fused noise 0.05 (C5's)."""
+at ENVS >= 32 per CU (or DIAG | 1024) the 32-env k_pg_rollout_e8.  Configs: easy, hard, easy + fused noise 0.05 (C5's)."""
 import os
 import sys
 

@@ -1,4 +1,4 @@
-"""Time the fused PG rollout kernels (ws default, ls = diag 64; ONE=1 adds the one-lane-per-env
+"""Time the fused PG rollout kernels (the default selection; ONE=1 adds the one-lane-per-env
 kernel, diag 16; DIAGS=flags:name,... picks them, e.g. 0:default,2048:ws16,1024:e8) at the bench
 shape (ENVS, default 4096; CUR the curriculum preset), one line."""
 import os
@@ -17,7 +17,7 @@ for noise in (0.0, 0.05):
     env = envs.VecEnv(int(os.environ.get("ENVS", "4096")), curriculum_config=pkg.CurriculumConfig.named(cur), reward_type="dense", seed=1, device=dev)
     tr = trainer.PGTrainer(env, trainer.TrainerConfig(horizon=200, seed=7, obs_noise_std=noise, dyn_noise_std=noise))
     env.reset(write_obs=False)
-    kernels = ((0, "ws"), (64, "ls")) + (((16, "one"),) if os.environ.get("ONE") else ())
+    kernels = ((0, "default"),) + (((16, "one"),) if os.environ.get("ONE") else ())
     if os.environ.get("DIAGS"):  # e.g. DIAGS=0:default,2048:ws16,1024:e8
         kernels = tuple((int(d.split(":")[0]), d.split(":")[1]) for d in os.environ["DIAGS"].split(","))
     for flags, name in kernels:

@@ -44,7 +44,10 @@ __device__ __forceinline__ double clipd(double x, double lo, double hi) {
 struct u32x4 {
     uint32_t x, y, z, w;
 };
-template <int kRounds = 10>
+#ifndef DXRL_PHILOX_ROUNDS
+#define DXRL_PHILOX_ROUNDS 10
+#endif
+template <int kRounds = DXRL_PHILOX_ROUNDS>
 __device__ __forceinline__ u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {

@@ -98,6 +98,9 @@ class TrainerConfig:
     # and both reductions in one launch (needs the fused learner with on-chip H1, serialised
     # exchanges, and > 16 row chunks per split); False: one dxrl_pg_fused call per network
     pair_learner: bool = True
+    # dW2 splits per network of the paired step (0: learner CUs / 2, capped by the smallest
+    # minibatch slice's 32-row chunks / 17)
+    pair_splits: int = 0
 
 
 def minibatch_bounds(M: int, B: int, round_samples: int):
@@ -244,7 +247,7 @@ class PGTrainer:
         # paired learner step (dxrl_pg_fused_pair): the critic's own dH2 / partial buffers, the
         # per-network dW2 split count (every minibatch slice must give each split > 16 chunks)
         mb_rows = min(b - a for a, b in zip(self.minibatch_bounds()[:-1], self.minibatch_bounds()[1:]))
-        self.pair_splits = min(self.learner_cus // 2, mb_rows // 32)
+        self.pair_splits = min(int(cfg.pair_splits) or self.learner_cus // 2, mb_rows // 32)
         self.paired = (cfg.pair_learner and cfg.fused and cfg.h1_recompute and self._comm is None
                        and self.pair_splits > 16 and all(x % 32 == 0 for x in self.minibatch_bounds()))
         self.dH2c = self.fused_partial_c = self.kpartial_c = self.kpartial_a = None

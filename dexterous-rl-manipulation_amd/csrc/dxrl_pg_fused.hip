@@ -341,6 +341,24 @@ __device__ __forceinline__ void copy_tile_out_n(const bf16* T, bf16* out, int64_
     }
 }
 
+// One 16-byte chunk of the dH2 tile to HBM.  Non-temporal (DXRL_DH2_NT, default): the line is
+// written through instead of staying dirty in the caches, so k_wgrad_l1's read-back of the 0.42
+// GB per network does not also pay for the write-back of the lines it evicts -- a 524 MB LDS-DMA
+// stream runs at 6.1 TB/s after nt stores and at 4.0 TB/s after plain, sc1 or sc0 sc1 stores
+// (tools/stream_mb.hip, profiles/r05/stream_after_store_policy.log).
+#ifndef DXRL_DH2_NT
+#define DXRL_DH2_NT 1
+#endif
+__device__ __forceinline__ void store_dh2(bf16* dst, const bf16x8& v) {
+    if (DXRL_DH2_NT) {
+        typedef unsigned int u32v4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(__builtin_bit_cast(u32v4, v),
+                                    (__attribute__((address_space(1))) u32v4*)dst);
+    } else {
+        *(__attribute__((address_space(1))) bf16x8*)dst = v;
+    }
+}
+
 // Hide a pointer's provenance from the optimiser so loads through it are not hoisted
 // out of the tile loop (loop-invariant weight / bias loads would otherwise pin registers
 // for the whole launch).
@@ -990,7 +1008,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 if (diag & 1 || sidx % kEvery != kEvery - 1) return;
                 const int c = tid_l + kFThreads * (sidx / kEvery), row = c >> 5, col = 8 * (c & 31);
                 const bf16x8 v = *reinterpret_cast<const bf16x8*>(H2 + row * kHp + col);
-                if (m0 + row < p.rows) *(__attribute__((address_space(1))) bf16x8*)(p.dh2_out + (m0 + row) * kH + col) = v;
+                if (m0 + row < p.rows) store_dh2(p.dh2_out + (m0 + row) * kH + col, v);
             };
             fwd_pipe<kH / 16, kHp, kMT>(pw2t, H2, lane, eg, NoHook{}, false, copy_k);
 #else

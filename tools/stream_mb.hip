@@ -9,10 +9,12 @@
 //         observation rows per chunk (four pieces from the first, one from the second per wave)
 //   dma2w dma2 right after the whole buffer was rewritten (as dH2 is by the pass before
 //         k_wgrad_l1: dirty lines in the caches when the stream starts)
+//   w-*   dma2 right after a kernel rewrote the buffer with plain / nt / sc1 / sc0 sc1 stores
 // hipcc --offload-arch=gfx950 -O3 tools/stream_mb.hip -o tools/stream_mb && ./tools/stream_mb
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 constexpr int kChunk = 20 * 1024, kRing = 4, kGrid = 256, kThreads = 512;
 
@@ -92,8 +94,28 @@ __global__ __launch_bounds__(kThreads, 1) void k_reg(const char* src, int64_t nc
     out[blockIdx.x * kThreads + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
 }
 
-int main() {
-    const int64_t bytes = 524LL * 1024 * 1024, nchunks = bytes / kChunk;
+// rewrite the buffer with 16-byte vector stores of one cache policy: 0 plain, 1 nt, 2 sc1,
+// 3 sc0 sc1 (what the producer of a streamed buffer can choose)
+template <int kPol>
+__global__ __launch_bounds__(256) void k_fill(uint4* dst, int64_t n16, uint32_t v) {
+    const uint4 x = make_uint4(v, v ^ 1u, v ^ 2u, v ^ 3u);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+        if (kPol == 0) dst[i] = x;
+        if (kPol == 1) {
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(v4u{x.x, x.y, x.z, x.w}, reinterpret_cast<v4u*>(dst + i));
+        }
+        typedef unsigned int v4r __attribute__((ext_vector_type(4)));
+        const v4r xr = {x.x, x.y, x.z, x.w};
+        if (kPol == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst + i), "v"(xr) : "memory");
+        if (kPol == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst + i), "v"(xr) : "memory");
+    }
+}
+
+int main(int argc, char** argv) {
+    // argv[1]: MiB streamed (default 524: k_wgrad_l1's bytes per network at C2); smaller sizes
+    // show what the memory-side cache (256 MiB) does for a buffer written just before
+    const int64_t bytes = (argc > 1 ? atoll(argv[1]) : 524LL) * 1024 * 1024, nchunks = bytes / kChunk;
     char* src;
     uint32_t* out;
     if (hipMalloc(&src, nchunks * kChunk) != hipSuccess || hipMalloc(&out, kGrid * kThreads * 4) != hipSuccess) return 1;
@@ -103,11 +125,20 @@ int main() {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    for (int v = 0; v < 5; ++v) {
+    for (int v = 0; v < 9; ++v) {
         float best = 1e9f;
         for (int rep = 0; rep < 6; ++rep) {
             if (v == 4) {
                 hipMemsetAsync(src, rep, nchunks * kChunk);
+                hipDeviceSynchronize();
+            }
+            if (v >= 5) {  // rewritten by a kernel with store policy v - 5
+                const int64_t n16 = nchunks * kChunk / 16;
+                uint4* d = reinterpret_cast<uint4*>(src);
+                if (v == 5) hipLaunchKernelGGL(k_fill<0>, dim3(2048), dim3(256), 0, 0, d, n16, (uint32_t)rep);
+                if (v == 6) hipLaunchKernelGGL(k_fill<1>, dim3(2048), dim3(256), 0, 0, d, n16, (uint32_t)rep);
+                if (v == 7) hipLaunchKernelGGL(k_fill<2>, dim3(2048), dim3(256), 0, 0, d, n16, (uint32_t)rep);
+                if (v == 8) hipLaunchKernelGGL(k_fill<3>, dim3(2048), dim3(256), 0, 0, d, n16, (uint32_t)rep);
                 hipDeviceSynchronize();
             }
             hipEventRecord(a);
@@ -121,7 +152,7 @@ int main() {
             hipEventElapsedTime(&ms, a, b);
             if (rep && ms < best) best = ms;
         }
-        printf("%-6s %8.1f us  %.2f TB/s\n", v == 0 ? "dma" : v == 1 ? "reg" : v == 2 ? "regnb" : v == 3 ? "dma2" : "dma2w", best * 1e3,
+        printf("%5lld MiB %-6s %8.1f us  %.2f TB/s\n", (long long)(bytes >> 20), v == 0 ? "dma" : v == 1 ? "reg" : v == 2 ? "regnb" : v == 3 ? "dma2" : v == 4 ? "dma2w" : v == 5 ? "w-plain" : v == 6 ? "w-nt" : v == 7 ? "w-sc1" : "w-sc01", best * 1e3,
                (double)nchunks * kChunk / (best * 1e-3) / 1e12);
     }
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;

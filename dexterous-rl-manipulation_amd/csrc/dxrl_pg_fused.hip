@@ -341,13 +341,14 @@ __device__ __forceinline__ void copy_tile_out_n(const bf16* T, bf16* out, int64_
     }
 }
 
-// One 16-byte chunk of the dH2 tile to HBM.  Non-temporal (DXRL_DH2_NT, default): the line is
-// written through instead of staying dirty in the caches, so k_wgrad_l1's read-back of the 0.42
-// GB per network does not also pay for the write-back of the lines it evicts -- a 524 MB LDS-DMA
-// stream runs at 6.1 TB/s after nt stores and at 4.0 TB/s after plain, sc1 or sc0 sc1 stores
-// (tools/stream_mb.hip, profiles/r05/stream_after_store_policy.log).
+// One 16-byte chunk of the dH2 tile to HBM, a plain store.  DXRL_DH2_NT=1 stores it non-temporal
+// (written through instead of left dirty in the caches, so k_wgrad_l1's read-back does not also
+// pay for the write-back of the lines it evicts: a 524 MB LDS-DMA stream runs at 6.1 TB/s after
+// nt stores and at 4.0 TB/s after plain ones, tools/stream_mb.hip).  Not the default: +1-1.7 % on
+// most boxes, -10 % on others, all kernels of the iteration slower there
+// (profiles/r05/ab_dh2_nt.log).
 #ifndef DXRL_DH2_NT
-#define DXRL_DH2_NT 1
+#define DXRL_DH2_NT 0
 #endif
 __device__ __forceinline__ void store_dh2(bf16* dst, const bf16x8& v) {
     if (DXRL_DH2_NT) {

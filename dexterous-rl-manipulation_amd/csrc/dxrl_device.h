@@ -68,9 +68,27 @@ __device__ __forceinline__ double u01_53(uint32_t hi, uint32_t lo) {
 }
 // 24-bit uniform in (0,1]
 __device__ __forceinline__ float u01_24(uint32_t v) { return ((float)(v >> 8) + 1.0f) * (1.0f / 16777216.0f); }
-// two standard normals (Box-Muller, f32) from two u32.  Network-noise math, not parity math (no
-// CPU restatement replays these values: parity runs replay the device's action tape): hardware
-// log, sqrt and sin / cos, no correctly rounded sequences.
+// Box-Muller on the hardware transcendentals, for uniforms u1 = (v + 1) 2^-kBits (v = the
+// kBits-bit integer of the first source, u1 formed exactly) and u2 (the angle in revolutions,
+// which v_sin_f32 / v_cos_f32 take directly): r = sqrt(-2 ln 2 log2 u1) with v_log_f32 (log2) of
+// u1 itself (log2 of v + 1 minus kBits would cancel near u1 = 1).  The same values as
+// sqrt(-2 __logf(u1)) and __sincosf(2 pi u2) up to the hardware approximations, in 12 vector
+// instructions + 4 transcendentals per pair instead of 23 + 4 (__logf is libm-accurate: a
+// denormal rescale and a two-term ln 2 product around its v_log_f32; __sincosf scales by 2 pi
+// and back).  The clamp keeps r real should log2 of u1 <= 1 round above zero.
+template <int kBits>
+__device__ __forceinline__ void box_muller_hw(uint32_t v, float u2_rev, float& n0, float& n1) {
+    constexpr float kM2Ln2 = -1.38629436111989061883f, kUlp = 1.0f / (float)(1u << kBits);
+    const float l = __builtin_amdgcn_logf((float)(v + 1u) * kUlp);
+    const float r = __builtin_amdgcn_sqrtf(fmaxf(l * kM2Ln2, 0.0f));
+    n0 = r * __builtin_amdgcn_cosf(u2_rev);
+    n1 = r * __builtin_amdgcn_sinf(u2_rev);
+}
+// two standard normals (Box-Muller, f32) from two u32 (24-bit uniforms in (0, 1]): the policy
+// noise.  Network-noise math, not parity math (no CPU restatement replays these values: parity
+// runs replay the device's action tape).  Kept on __logf / __sincosf: box_muller_hw<24> here
+// made the C2 rollout 1.2-1.8 % slower (its draws run in the head phase beside the mu head) while
+// the fused noise gained from it (profiles/r05/ab_box_muller.log)
 __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& n0, float& n1) {
     const float r = __builtin_amdgcn_sqrtf(-2.0f * __logf(u01_24(a)));
     float s, c;
@@ -100,7 +118,8 @@ constexpr uint32_t kStreamReset = 0x52535400u, kStreamPolicy = 0x504f4c00u, kStr
 //      counter (lo ctr, hi ctr << 8 ^ stream ^ blk) under the key k0 ^ k1 * 0x9E3779B9, and
 //      Box-Muller over the 16-bit halves of each output word ((lo, hi) of word 0, then of word 1):
 //      half the 64-bit products per normal.  Config C5 rollout / C2 rollout 1.15 -> 1.12 (A/B,
-//      profiles/r05/ab_c5_noise_generators.log).
+//      profiles/r05/ab_c5_noise_generators.log); Box-Muller on the hardware transcendentals
+//      (box_muller_hw, same definition): 1.12 -> 1.10 (profiles/r05/ab_box_muller.log).
 // oracle/dx_oracle.py device_normals_f64 restates both.
 #ifndef DXRL_NOISE_GEN
 #define DXRL_NOISE_GEN 1
@@ -116,14 +135,11 @@ __device__ __forceinline__ void philox2x32_10(uint32_t& c0, uint32_t& c1, uint32
         k += 0x9E3779B9u;
     }
 }
-// 16-bit uniform in (0, 1]
-__device__ __forceinline__ float u01_16(uint32_t v) { return ((float)v + 1.0f) * (1.0f / 65536.0f); }
 __device__ __forceinline__ void box_muller16(uint32_t w, float& n0, float& n1) {
-    const float r = __builtin_amdgcn_sqrtf(-2.0f * __logf(u01_16(w & 0xFFFFu)));
-    float s, c;
-    __sincosf(6.28318530717958647692f * u01_16(w >> 16), &s, &c);
-    n0 = r * c;
-    n1 = r * s;
+    // u2 = (hi + 1) 2^-16 as 1 + (hi + 1) 2^-16 revolutions (one period on): the bits of hi
+    // placed in the mantissa of 1.0 and 2^-16 added, both exact
+    const float rev = __uint_as_float(0x3F800000u | ((w >> 16) << 7)) + (1.0f / 65536.0f);
+    box_muller_hw<16>(w & 0xFFFFu, rev, n0, n1);
 }
 __device__ __forceinline__ void noise_normals4(uint64_t ctr, uint32_t stream, uint32_t blk, uint32_t k0, uint32_t k1,
                                                float nz[4]) {

@@ -1,6 +1,8 @@
 # A/B of the Box-Muller implementation (hardware log2 / sin / cos in revolutions vs __logf /
 # __sincosf): GPU tests on the new library, rollout-time ratios (C2 easy, C5 variable + noise,
 # C4 hard at 8192 envs) and C2 / C5 bench lines, interleaved on one box
+# Libraries first: SRC_REV=<commit before the change> python tools/build_variant.py bmold;
+#   python tools/build_variant.py bmnew
 set -o pipefail
 O=gpurun_out/bm
 mkdir -p $O

@@ -1,4 +1,7 @@
 # A/B of the dH2 store policy on one box: bench lines only (C2), three interleaved rounds
+# Libraries first (here): printf '#define DXRL_DH2_NT 0' > o; printf '#define DXRL_DH2_NT 1' > n;
+#   python tools/build_variant.py dh2nt dxrl_pg_fused.hip o n; python tools/build_variant.py dh2plain
+#   then on the box: VARS="dh2plain dh2nt" bash tools/ab_dh2_bench.sh (VARS: any ab/lib<V>.so names)
 set -o pipefail
 O=gpurun_out/ntb
 mkdir -p $O

@@ -1,4 +1,5 @@
 # A/B of the dH2 store policy on one box: plain bench lines, then rocprofv3 kernel stats (C2)
+# Libraries first: ab/libdh2nt.so and ab/libdh2plain.so as in tools/ab_dh2_bench.sh
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/ntprof

@@ -247,6 +247,8 @@ class PGTrainer:
         # paired learner step (dxrl_pg_fused_pair): the critic's own dH2 / partial buffers, the
         # per-network dW2 split count (every minibatch slice must give each split > 16 chunks)
         mb_rows = min(b - a for a, b in zip(self.minibatch_bounds()[:-1], self.minibatch_bounds()[1:]))
+        if int(cfg.pair_splits) < 0:
+            raise ValueError("pair_splits must be >= 0 (0: learner CUs / 2)")
         self.pair_splits = min(int(cfg.pair_splits) or self.learner_cus // 2, mb_rows // 32)
         self.paired = (cfg.pair_learner and cfg.fused and cfg.h1_recompute and self._comm is None
                        and self.pair_splits > 16 and all(x % 32 == 0 for x in self.minibatch_bounds()))

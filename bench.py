@@ -60,9 +60,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--prewarm-s", type=float, default=1.0,
+    p.add_argument("--prewarm-s", type=float, default=2.0,
                    help="untimed iterations for at least this long before the --warmup ones: the GPU's clocks "
-                        "take the first ~0.1-1 s of work to reach their sustained level (DESIGN.md §6)")
+                        "take the first ~1-2 s of work to reach their sustained level (DESIGN.md §6)")
     p.add_argument("--config", choices=sorted(WORKLOADS), default="easy",
                    help="BASELINE configs[1..4]: easy (C2, the metric's config), default (C3: curriculum "
                         "scheduler), hard_heldout (C4: held-out object table, 8192 envs), variable_noise (C5)")

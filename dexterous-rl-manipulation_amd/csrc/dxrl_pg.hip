@@ -497,6 +497,13 @@ struct WsReward {      // an env's dense-reward inputs and episode end of one st
 #ifndef DXRL_WS_PRIO
 #define DXRL_WS_PRIO -1  // -1: by instantiation (env waves first with fused noise)
 #endif
+// Observation row t + 1 written at the end of step t's P4 instead of in step t + 1's P0 (no P0
+// phase, no barrier for it) -- in the instantiations without fused noise only: there the rollout
+// runs 1 % faster; with fused noise the aux waves' P0 draw stays and the env lanes' longer P4
+// (the row's noise add) made it 7 % slower (profiles/r05/ab_ws_obs_in_p4.log)
+#ifndef DXRL_WS_OBS_IN_P4
+#define DXRL_WS_OBS_IN_P4 1
+#endif
 template <bool kNoise, bool kDiag>
 __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p) {
     constexpr int kRows = 32;
@@ -524,6 +531,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
     // +1 % (so they keep equal priorities); aux first or per-phase priorities lose 5-10 %
     // (rollout_time A/B, profiles/r04/ab_rollout_wave_priority.log)
     constexpr int kPrio = DXRL_WS_PRIO >= 0 ? DXRL_WS_PRIO : (kNoise ? 1 : 0);
+    constexpr bool kObsInP4 = DXRL_WS_OBS_IN_P4 != 0 && !kNoise;
     if (kPrio != 0 && (__builtin_amdgcn_readfirstlane(wave) >= 4) == (kPrio == 2))
         __builtin_amdgcn_s_setprio(1);
     const int et_tid = tid & 255;  // the env lane this thread is (env wave) or twins (aux wave)
@@ -918,17 +926,24 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         }                                                                                        \
     } while (0)
     if (aux && live) obs_draws(p.iteration * (uint64_t)T, 0);
+    // kObsInP4: observation row t + 1 is written by the env lanes at the end of step t's P4
+    // (right after the state it shows), so step t + 1 opens with layer 1 -- no P0 phase and no
+    // barrier for it (row 0 here, before the first one)
+    if (kObsInP4) {
+        __syncthreads();  // row 0's noise (drawn just above) visible
+        if (!aux && live) write_obs_row(0);
+    }
     __syncthreads();
     WS_STAMP(7);
     for (int64_t t = 0; t < T; ++t) {
         const int64_t m = t * n + i;
         const uint64_t ctr = p.iteration * (uint64_t)T + (uint64_t)t;
-        if (!aux && live) write_obs_row((int)(t & 1));
+        if (!kObsInP4 && !aux && live) write_obs_row((int)(t & 1));
         // the next observation row's noise (aux lanes, own rows; counter-only, so drawn here where
         // the aux waves wait for the env lanes' row, not in the head phase beside the draws)
         if (aux && live && (!kDiag || !(p.diag & 256))) obs_draws(ctr + 1, (int)((t + 1) & 1), true, ctr);
         WS_STAMP(0);
-        lds_barrier();
+        if (!kObsInP4) lds_barrier();
         if (!aux && live) tape_obs_row(m);
         if (mlp) wave_layer16<kIn / 32, 2, false, true>(X, kXsW, w1frag, 32 * wave, H1, kHsW, lane);  // b: col 45
         WS_STAMP(1);
@@ -974,6 +989,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
                 if (t > 0 && env_on && !(kDiag && (p.diag & 512))) settle(t - 1);  // step t-1's reward and bookkeeping
             } else {
                 env_lane_step(t, m);
+                if (kObsInP4) write_obs_row((int)((t + 1) & 1));  // row t + 1 (row T: the bootstrap)
             }
         }
         WS_STAMP(5);
@@ -998,8 +1014,9 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
         }
     }
     if (live && !aux) {
-        // bootstrap observation (slot T), then the state back to the slab
-        write_obs_row((int)(T & 1));
+        // bootstrap observation (slot T; with kObsInP4 already written by the last step's P4),
+        // then the state back to the slab
+        if (!kObsInP4 || T == 0) write_obs_row((int)(T & 1));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         tape_obs_row(T * n + i);

@@ -175,6 +175,9 @@ _SIGS = {
     "dxrl_pg_fused_sizes": (C.c_int, [C.POINTER(_I32), C.POINTER(_I64)]),
     "dxrl_pg_fused": (C.c_int, [_I32, C.POINTER(PgFusedArgs), _P]),
     "dxrl_pg_fused_pair": (C.c_int, [_I32, C.POINTER(PgFusedArgs), C.POINTER(PgFusedArgs), _P]),
+    "dxrl_pg_fused_pair_gnorm": (C.c_int, [_I32, C.POINTER(PgFusedArgs), C.POINTER(PgFusedArgs), _P, _I32,
+                                           C.POINTER(_I32), _P]),
+    "dxrl_pg_gnorm_blocks": (C.c_int, [C.POINTER(_I32)]),
     "dxrl_evaluate": (C.c_int, [_P, C.POINTER(EvalArgs), _P]),
     "dxrl_sched_scratch_bytes": (C.c_int, [_I32, _I32, _I64, _I32, C.POINTER(_I64)]),
     "dxrl_sched_scan": (C.c_int, [_I32, C.POINTER(SchedArgs), _P]),
@@ -187,6 +190,8 @@ _SIGS = {
     "dxrl_pg_adam": (C.c_int, [_I32, _P, _P, _P, _P, _I64, _F64, _F64, _F64, _F64, _I64, _P, _F64, _P]),
     "dxrl_pg_optimizer_step": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P, _I64, _F64, _F64, _F64, _F64, _I64, _F64,
                                          _P, _P, _P, _P]),
+    "dxrl_pg_adam_step": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P, _I64, _F64, _F64, _F64, _F64, _I64, _F64, _P,
+                                    _I32, _P, _P, _P]),
 }
 
 _lib = None

@@ -91,9 +91,11 @@ __device__ __forceinline__ float4 ordered_slab_sum(const float4* __restrict__ pa
 // One 256-thread block of the two-level fixed-order slab sum (k_slab_reduce2_4): float4 columns
 // 16 blk .. 16 blk + 15 of z slabs; 16 groups of threads sum contiguous slab ranges, then group 0
 // adds the 16 group sums in group order.  grp: the block's [16][16] float4 scratch in LDS.
-__device__ __forceinline__ void slab_reduce_block(const float4* __restrict__ partial, int64_t slab4, int z,
-                                                  float* __restrict__ out, int accumulate, int cols, int64_t ldo,
-                                                  int64_t blk, float4 (*grp)[16]) {
+// Returns the thread's f64 sum of squares of the four values it stored (0 on the other threads;
+// unused by callers that do not need a norm, so the compiler drops it there).
+__device__ __forceinline__ double slab_reduce_block(const float4* __restrict__ partial, int64_t slab4, int z,
+                                                    float* __restrict__ out, int accumulate, int cols, int64_t ldo,
+                                                    int64_t blk, float4 (*grp)[16]) {
     constexpr int kRX = 16;
     const int x = threadIdx.x % kRX, g = threadIdx.x / kRX;
     const int64_t i = blk * kRX + x;
@@ -102,7 +104,7 @@ __device__ __forceinline__ void slab_reduce_block(const float4* __restrict__ par
     if (i < slab4) s = ordered_slab_sum(partial, slab4, i, k0, k1, s);
     grp[g][x] = s;
     __syncthreads();
-    if (g != 0 || i >= slab4) return;
+    if (g != 0 || i >= slab4) return 0.0;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
     for (int q = 0; q < kReduceGroups; ++q) {
@@ -120,6 +122,7 @@ __device__ __forceinline__ void slab_reduce_block(const float4* __restrict__ par
         r = make_float4(a.x + r.x, a.y + r.y, a.z + r.z, a.w + r.w);
     }
     *dst = r;
+    return (((double)r.x * r.x + (double)r.y * r.y) + (double)r.z * r.z) + (double)r.w * r.w;
 }
 
 }  // namespace dxrl

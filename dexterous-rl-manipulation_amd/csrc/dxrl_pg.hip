@@ -1840,6 +1840,23 @@ int dxrl_pg_optimizer_step(int32_t device, const float* params, const float* gra
     return launch_check("k_adam_pack");
 }
 
+int dxrl_pg_adam_step(int32_t device, const float* params, const float* grads, const float* m1, const float* m2,
+                      float* params_out, float* m1_out, float* m2_out, int64_t n, double lr, double beta1, double beta2,
+                      double eps, int64_t step, double max_norm, const double* gnorm_partial, int32_t gnorm_blocks,
+                      double* gnorm2, void* packed, void* stream) {
+    DXRL_REQUIRE(params && grads && m1 && m2 && params_out && m1_out && m2_out && gnorm_partial && gnorm2 && packed &&
+                     step >= 1 && gnorm_blocks >= 1,
+                 "bad adam_step arguments");
+    DXRL_REQUIRE(n == kParams, "adam_step: n must be the padded parameter count %lld", (long long)kParams);
+    DXRL_REQUIRE(params != params_out && m1 != m1_out && m2 != m2_out, "adam_step: outputs must not alias inputs");
+    DeviceGuard g(device);
+    AdamPackArgs a{params, grads, m1, m2, params_out, m1_out, m2_out, n, (float)lr, (float)beta1, (float)beta2,
+                   (float)eps, (float)(1.0 - pow(beta1, (double)step)), (float)(1.0 - pow(beta2, (double)step)),
+                   (float)max_norm, gnorm_partial, gnorm_blocks, gnorm2, static_cast<bf16*>(packed)};
+    hipLaunchKernelGGL(k_adam_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), a);
+    return launch_check("k_adam_pack");
+}
+
 int dxrl_pg_adam(int32_t device, float* params, const float* grads, float* m1, float* m2, int64_t n, double lr,
                  double beta1, double beta2, double eps, int64_t step, const double* gnorm2, double max_norm,
                  void* stream) {

@@ -1184,22 +1184,25 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
 }
 
 // One element of the grads blocks W1 / W3 / log_std (actor) / W2's column 256 + pads from the
-// workgroup sum s = sum[j] (k_fused_scatter's mapping; `j` indexes the partial-slab layout)
-__device__ __forceinline__ void fused_scatter_one(int j, float s, float* __restrict__ gW1, float* __restrict__ gW3,
-                                                  float* __restrict__ gLs, float* __restrict__ gW2, float ent_coef) {
+// workgroup sum s = sum[j] (k_fused_scatter's mapping; `j` indexes the partial-slab layout).
+// Returns the value stored into the gradient element slab entry j maps to (0 when it maps to
+// none; the pads it zeroes contribute nothing to a norm).
+__device__ __forceinline__ float fused_scatter_one(int j, float s, float* __restrict__ gW1, float* __restrict__ gW3,
+                                                   float* __restrict__ gLs, float* __restrict__ gW2, float ent_coef) {
     if (j >= kPartB2) {  // W2 block column 256 (bias) and the zero pad columns 257..287 of row n
         const int n = j - kPartB2;
         if (n < kH) {
             gW2[(int64_t)n * kHx + kH] = s;
             for (int c = kH + 1; c < kHx; ++c) gW2[(int64_t)n * kHx + c] = 0.0f;
+            return s;
         }
-        return;
+        return 0.0f;
     }
     if (j < kPartW3) {  // dW1 [256][64]: columns 0..47 from the slab, 48..63 zero
         const int row = j / kPW1C, col = j % kPW1C;
         gW1[row * kIn + col] = s;
         if (col < kIn - kPW1C) gW1[row * kIn + kPW1C + col] = 0.0f;
-        return;
+        return s;
     }
     if (j < kPartLs) {  // dW3 [32][288]: rows 0..15 columns 0..256 from the slab, the rest zero
         const int o = (j - kPartW3) / kPW3C, col = (j - kPartW3) % kPW3C;
@@ -1210,23 +1213,32 @@ __device__ __forceinline__ void fused_scatter_one(int j, float s, float* __restr
             for (int c = kH + 1; c < kHx; ++c) gW3[o * kHx + c] = 0.0f;
             for (int c = kH; c < kHx; ++c) gW3[(16 + o) * kHx + c] = 0.0f;
         }
-        return;
+        return col <= kH ? s : 0.0f;
     }
     if (gLs) {
         const int k = j - kPartLs;
-        gLs[k] = k < kAct ? s - ent_coef : 0.0f;
+        const float v = k < kAct ? s - ent_coef : 0.0f;
+        gLs[k] = v;
+        return v;
     }
+    return 0.0f;
+}
+
+// f64 squares of four stored gradient values, summed in one fixed order
+__device__ __forceinline__ double sumsq4(float a, float b, float c, float d) {
+    return (((double)a * a + (double)b * b) + (double)c * c) + (double)d * d;
 }
 
 // The workgroup partials summed and scattered in one launch: a 256-thread block owns 16 float4
 // columns of the [z][kPartSize] slabs; with z > kReduceGroups thread (g, x) sums group g's slabs
 // of column x in order and the 16 group sums are added in group order (launch_slab_reduce's two
 // levels), else one thread sums the z slabs in order (its one level) -- the same per-element order
-// either way -- and the column goes straight into the grads blocks.
-__device__ __forceinline__ void fused_reduce_block(const float4* __restrict__ partial, int z, float* __restrict__ gW1,
-                                                   float* __restrict__ gW3, float* __restrict__ gLs,
-                                                   float* __restrict__ gW2, float ent_coef, int64_t blk,
-                                                   float4 (*grp)[16]) {
+// either way -- and the column goes straight into the grads blocks.  Returns the thread's f64 sum
+// of squares of the gradient values it stored (0 on threads that store none).
+__device__ __forceinline__ double fused_reduce_block(const float4* __restrict__ partial, int z, float* __restrict__ gW1,
+                                                     float* __restrict__ gW3, float* __restrict__ gLs,
+                                                     float* __restrict__ gW2, float ent_coef, int64_t blk,
+                                                     float4 (*grp)[16]) {
     constexpr int kRX = 16;
     constexpr int64_t kSlab4 = kPartSize / 4;
     static_assert(kPartSize % 4 == 0 && 256 == kRX * kReduceGroups, "layout");
@@ -1240,18 +1252,19 @@ __device__ __forceinline__ void fused_reduce_block(const float4* __restrict__ pa
         if (i < kSlab4) s = ordered_slab_sum(partial, kSlab4, i, k0, k1, s);  // == the in-order loop
         grp[g][x] = s;
         __syncthreads();
-        if (g != 0 || i >= kSlab4) return;
+        if (g != 0 || i >= kSlab4) return 0.0;
 #pragma unroll
         for (int q = 0; q < kReduceGroups; ++q) r = add(r, grp[q][x]);
     } else {
-        if (g != 0 || i >= kSlab4) return;
+        if (g != 0 || i >= kSlab4) return 0.0;
         r = ordered_slab_sum(partial, kSlab4, i, 0, z, r);
     }
     const int j = (int)(4 * i);
-    fused_scatter_one(j, r.x, gW1, gW3, gLs, gW2, ent_coef);
-    fused_scatter_one(j + 1, r.y, gW1, gW3, gLs, gW2, ent_coef);
-    fused_scatter_one(j + 2, r.z, gW1, gW3, gLs, gW2, ent_coef);
-    fused_scatter_one(j + 3, r.w, gW1, gW3, gLs, gW2, ent_coef);
+    const float v0 = fused_scatter_one(j, r.x, gW1, gW3, gLs, gW2, ent_coef);
+    const float v1 = fused_scatter_one(j + 1, r.y, gW1, gW3, gLs, gW2, ent_coef);
+    const float v2 = fused_scatter_one(j + 2, r.z, gW1, gW3, gLs, gW2, ent_coef);
+    const float v3 = fused_scatter_one(j + 3, r.w, gW1, gW3, gLs, gW2, ent_coef);
+    return sumsq4(v0, v1, v2, v3);
 }
 
 __global__ __launch_bounds__(256) void k_fused_reduce_scatter(const float4* __restrict__ partial, int z,
@@ -1288,13 +1301,27 @@ struct GradReduceNet {
     int64_t ldo;
     int nb1, nb2;
 };
-__global__ __launch_bounds__(256) void k_grad_reduce_nets(GradReduceNet a, GradReduceNet b) {
+// gn (optional): gn[block] = the f64 sum of squares of every gradient value the block stored, in
+// one fixed order (a butterfly inside each wave, then the four wave sums in wave order).  The
+// blocks together store every element of the master-layout gradient (pads as zeros), so at one
+// rank these partials are the global norm's: the optimiser step reads them instead of running
+// k_sumsq over the finished gradient (dxrl_pg_fused_pair_gnorm + dxrl_pg_adam_step).
+__global__ __launch_bounds__(256) void k_grad_reduce_nets(GradReduceNet a, GradReduceNet b, double* __restrict__ gn) {
     __shared__ float4 grp[kReduceGroups][16];
+    __shared__ double red4[4];
     const bool second = (int)blockIdx.x >= a.nb1 + a.nb2;
     const GradReduceNet& r = second ? b : a;
     const int64_t blk = second ? (int64_t)blockIdx.x - (a.nb1 + a.nb2) : (int64_t)blockIdx.x;
-    if (blk < r.nb1) fused_reduce_block(r.fpart, r.fz, r.gW1, r.gW3, r.gLs, r.gW2, r.ent_coef, blk, grp);
-    else slab_reduce_block(r.wpart, (int64_t)kH * kH / 4, r.wz, r.gW2, 0, kH, r.ldo, blk - r.nb1, grp);
+    double q;
+    if (blk < r.nb1) q = fused_reduce_block(r.fpart, r.fz, r.gW1, r.gW3, r.gLs, r.gW2, r.ent_coef, blk, grp);
+    else q = slab_reduce_block(r.wpart, (int64_t)kH * kH / 4, r.wz, r.gW2, 0, kH, r.ldo, blk - r.nb1, grp);
+    if (gn) {  // launch-uniform; every thread of the block is still here
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+        if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = q;
+        __syncthreads();
+        if (threadIdx.x == 0) gn[blockIdx.x] = ((red4[0] + red4[1]) + red4[2]) + red4[3];
+    }
 }
 
 // grads blocks W1 / W3 (and log_std for the actor) from the workgroup sum (launch_slab_reduce)
@@ -1404,7 +1431,13 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
 }
 
 int dxrl_pg_fused_pair(int32_t device, const dxrl_pg_fused_args* c, const dxrl_pg_fused_args* a, void* stream) {
+    return dxrl_pg_fused_pair_gnorm(device, c, a, nullptr, 0, nullptr, stream);
+}
+
+int dxrl_pg_fused_pair_gnorm(int32_t device, const dxrl_pg_fused_args* c, const dxrl_pg_fused_args* a,
+                             double* gnorm_partial, int32_t gnorm_capacity, int32_t* gnorm_blocks, void* stream) {
     DXRL_REQUIRE(c && a, "fused_pair: null arguments");
+    DXRL_REQUIRE(!gnorm_partial || gnorm_blocks, "fused_pair: gnorm_partial needs gnorm_blocks");
     DXRL_REQUIRE(c->net == 1 && a->net == 0 && c->train && a->train, "fused_pair: a critic and an actor train pass");
     DXRL_REQUIRE(c->rows == a->rows && c->rows > 0 && c->rows % 32 == 0 && c->obs == a->obs && c->packed == a->packed &&
                      c->grads == a->grads && c->params == a->params,
@@ -1442,14 +1475,25 @@ int dxrl_pg_fused_pair(int32_t device, const dxrl_pg_fused_args* c, const dxrl_p
         return rc;
     DXRL_REQUIRE(ns_c > kReduceGroups && ns_a > kReduceGroups, "fused_pair: too few rows for the splits");
     const int nb1 = (int)((kPartSize / 4 + 15) / 16), nb2 = kH * kH / 4 / 16;
+    if (gnorm_partial) {
+        DXRL_REQUIRE(gnorm_capacity >= 2 * (nb1 + nb2), "fused_pair: gnorm_partial needs %d doubles", 2 * (nb1 + nb2));
+        *gnorm_blocks = 2 * (nb1 + nb2);
+    }
     GradReduceNet rc_{reinterpret_cast<const float4*>(c->partial), grid_c, G + kOffW1c, G + kOffW3c, nullptr,
                       G + kOffW2c, (float)c->ent_coef, reinterpret_cast<const float4*>(c->wgrad_partial), ns_c,
                       (int64_t)kHx, nb1, nb2};
     GradReduceNet ra_{reinterpret_cast<const float4*>(a->partial), grid_a, G + kOffW1a, G + kOffW3a, G + kOffLogStd,
                       G + kOffW2a, (float)a->ent_coef, reinterpret_cast<const float4*>(a->wgrad_partial), ns_a,
                       (int64_t)kHx, nb1, nb2};
-    hipLaunchKernelGGL(k_grad_reduce_nets, dim3((unsigned)(2 * (nb1 + nb2))), dim3(256), 0, st, rc_, ra_);
+    hipLaunchKernelGGL(k_grad_reduce_nets, dim3((unsigned)(2 * (nb1 + nb2))), dim3(256), 0, st, rc_, ra_,
+                       gnorm_partial);
     return launch_check("k_grad_reduce_nets");
+}
+
+int dxrl_pg_gnorm_blocks(int32_t* blocks) {
+    DXRL_REQUIRE(blocks, "null output");
+    *blocks = (int32_t)(2 * ((kPartSize / 4 + 15) / 16 + kH * kH / 4 / 16));
+    return DXRL_OK;
 }
 
 }  // extern "C"

@@ -101,6 +101,11 @@ class TrainerConfig:
     # dW2 splits per network of the paired step (0: learner CUs / 2, capped by the smallest
     # minibatch slice's 32-row chunks / 17)
     pair_splits: int = 0
+    # one rank, paired step: the pair's reduction also writes the grad-norm partials
+    # (dxrl_pg_fused_pair_gnorm) and the optimiser step finishes the norm from them
+    # (dxrl_pg_adam_step) instead of a k_sumsq pass over the gradient -- one launch fewer per
+    # update; the norm's f64 sum order differs (agrees to f64 rounding)
+    fused_gnorm: bool = True
 
 
 def minibatch_bounds(M: int, B: int, round_samples: int):
@@ -258,6 +263,13 @@ class PGTrainer:
             self.fused_partial_c = z(self.fused_grid + 17, pf_.value)
             self.kpartial_a = z(self.pair_splits, H, H)
             self.kpartial_c = z(self.pair_splits, H, H)
+        # grad-norm partials of the last paired step's reduction (one rank only: sharded, the
+        # all-reduce changes the gradient after them); _gn_blocks > 0 while they match the grads
+        self.gn_partial, self._gn_blocks = None, 0
+        if self.paired and cfg.fused_gnorm and not self.collective:
+            nbk = C.c_int32()
+            N.call("dxrl_pg_gnorm_blocks", C.byref(nbk))
+            self.gn_partial = torch.zeros(nbk.value, dtype=torch.float64, device=d)
         self.pack()
 
     # ------------------------------------------------------------------ params
@@ -371,7 +383,13 @@ class PGTrainer:
         fc.dh2, fc.partial, fc.wgrad_partial = p(self.dH2c), p(self.fused_partial_c), p(self.kpartial_c)
         fa.wgrad_partial = p(self.kpartial_a)
         fc.wgrad_splits = fa.wgrad_splits = self.pair_splits
-        N.call("dxrl_pg_fused_pair", self.dev.index, C.byref(fc), C.byref(fa), self._s())
+        if self.gn_partial is not None:
+            nb = C.c_int32()
+            N.call("dxrl_pg_fused_pair_gnorm", self.dev.index, C.byref(fc), C.byref(fa), p(self.gn_partial),
+                   self.gn_partial.numel(), C.byref(nb), self._s())
+            self._gn_blocks = nb.value
+        else:
+            N.call("dxrl_pg_fused_pair", self.dev.index, C.byref(fc), C.byref(fa), self._s())
 
     def critic_values(self):
         """V over the T + 1 observation blocks (fused forward, nothing stored but V)."""
@@ -380,6 +398,7 @@ class PGTrainer:
     def actor_train(self):
         start, rows = self._mb
         self._loss_rows = rows
+        self._gn_blocks = 0  # this pass rewrites the gradient: the pair's norm partials are stale
         if self._stats_pending:  # the actor's head normalises the advantages with the global moments
             # only the moments: the critic half's all-reduce queued behind them on the comm stream
             # runs beside this pass
@@ -390,6 +409,7 @@ class PGTrainer:
     def critic_train(self):
         start, rows = self._mb
         self._loss_rows = rows
+        self._gn_blocks = 0
         N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(1, True, rows, start)), self._s())
         # the critic half's SUM all-reduce runs beside the actor's pass -- only when an optimiser
         # step follows (iteration(update=False) issues no gradient collective, as the serialised
@@ -506,10 +526,17 @@ class PGTrainer:
         if self._spare is None:
             self._spare = tuple(torch.empty_like(t) for t in (self.params, self.m1, self.m2))
         po, m1o, m2o = self._spare
-        N.call("dxrl_pg_optimizer_step", self.dev.index, N.ptr(self.params), N.ptr(self.grads), N.ptr(self.m1),
-               N.ptr(self.m2), N.ptr(po), N.ptr(m1o), N.ptr(m2o), NPARAMS, c.lr, c.betas[0], c.betas[1], c.adam_eps,
-               self.step_count, c.max_grad_norm, N.ptr(self.partial), N.ptr(self.gnorm2), N.ptr(self.packed),
-               self._s())
+        if self._gn_blocks:  # one rank: the paired reduction left the norm's partials (no k_sumsq)
+            N.call("dxrl_pg_adam_step", self.dev.index, N.ptr(self.params), N.ptr(self.grads), N.ptr(self.m1),
+                   N.ptr(self.m2), N.ptr(po), N.ptr(m1o), N.ptr(m2o), NPARAMS, c.lr, c.betas[0], c.betas[1],
+                   c.adam_eps, self.step_count, c.max_grad_norm, N.ptr(self.gn_partial), self._gn_blocks,
+                   N.ptr(self.gnorm2), N.ptr(self.packed), self._s())
+            self._gn_blocks = 0
+        else:
+            N.call("dxrl_pg_optimizer_step", self.dev.index, N.ptr(self.params), N.ptr(self.grads), N.ptr(self.m1),
+                   N.ptr(self.m2), N.ptr(po), N.ptr(m1o), N.ptr(m2o), NPARAMS, c.lr, c.betas[0], c.betas[1],
+                   c.adam_eps, self.step_count, c.max_grad_norm, N.ptr(self.partial), N.ptr(self.gnorm2),
+                   N.ptr(self.packed), self._s())
         self._spare = (self.params, self.m1, self.m2)
         self.params, self.m1, self.m2 = po, m1o, m2o
 

@@ -442,6 +442,15 @@ int dxrl_pg_optimizer_step(int32_t device, const float* params, const float* gra
                            float* params_out, float* m1_out, float* m2_out, int64_t n, double lr, double beta1,
                            double beta2, double eps, int64_t step, double max_norm, double* partial, double* gnorm2,
                            void* packed, void* stream);
+/* dxrl_pg_optimizer_step's second launch alone: the grad norm is finished from gnorm_blocks f64
+ * partials the caller already holds (dxrl_pg_fused_pair_gnorm's, when one rank's reduction wrote
+ * the whole gradient) instead of a k_sumsq pass over the gradient.  Same Adam / pack arithmetic;
+ * the norm's f64 sum runs in another order, so it agrees with dxrl_pg_optimizer_step's to f64
+ * rounding, not bit for bit.  New learner, no reference counterpart. */
+int dxrl_pg_adam_step(int32_t device, const float* params, const float* grads, const float* m1, const float* m2,
+                      float* params_out, float* m1_out, float* m2_out, int64_t n, double lr, double beta1, double beta2,
+                      double eps, int64_t step, double max_norm, const double* gnorm_partial, int32_t gnorm_blocks,
+                      double* gnorm2, void* packed, void* stream);
 
 /* ---- fused one-pass learner step (csrc/dxrl_pg_fused.hip) ----------------------------
  * One launch per network replaces forward GEMMs + heads + backward GEMMs of the
@@ -488,6 +497,15 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* args, void* stream);
  * No reference counterpart (policies/simple_learner.py:73-95 is the update it replaces). */
 int dxrl_pg_fused_pair(int32_t device, const dxrl_pg_fused_args* critic, const dxrl_pg_fused_args* actor,
                        void* stream);
+/* dxrl_pg_fused_pair whose reduction also writes the global grad norm's partials: one f64 per
+ * reduction block (*gnorm_blocks of them, dxrl_pg_gnorm_blocks(); gnorm_capacity >= that), each
+ * the sum of squares of the gradient values the block stored.  The gradients are bit for bit
+ * dxrl_pg_fused_pair's.  At one rank the pair writes the whole gradient, so
+ * dxrl_pg_adam_step(gnorm_partial) replaces dxrl_pg_optimizer_step's k_sumsq launch; with a
+ * gradient all-reduce in between, the partials are stale and the caller uses the latter. */
+int dxrl_pg_fused_pair_gnorm(int32_t device, const dxrl_pg_fused_args* critic, const dxrl_pg_fused_args* actor,
+                             double* gnorm_partial, int32_t gnorm_capacity, int32_t* gnorm_blocks, void* stream);
+int dxrl_pg_gnorm_blocks(int32_t* blocks);
 
 /* ------------------------------------------------------------------------
  * Evaluation episode programs:

@@ -1298,9 +1298,19 @@ __device__ __forceinline__ double block_sum256(double s, double* red4) {
     __syncthreads();
     return ((red4[0] + red4[1]) + red4[2]) + red4[3];
 }
+// (thread t adds partial[t], partial[t + 256], ... in that order; the loads go out in batches of 8
+// ahead of their adds -- one L2 latency per batch, not per partial, for the ~2.6 k partials of
+// dxrl_pg_fused_pair_gnorm -- and the + 0.0 of a batch's tail leaves the sum's bits unchanged)
 __device__ __forceinline__ double block_sum_partials(const double* __restrict__ partial, int nb, double* red4) {
+    constexpr int kB = 8;
     double s = 0.0;
-    for (int k = threadIdx.x; k < nb; k += 256) s += partial[k];
+    for (int k0 = threadIdx.x; k0 < nb; k0 += 256 * kB) {
+        double v[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) v[u] = k0 + 256 * u < nb ? partial[k0 + 256 * u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < kB; ++u) s += v[u];
+    }
     return block_sum256(s, red4);
 }
 

@@ -1126,15 +1126,26 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(const float* __restrict__ r
 // everything but the recurrence itself taken off the serial chain.  A 256-thread workgroup owns
 // 16 envs:
 //   1. all 256 threads load the envs' whole horizon (rew, V_t, V_{t+1}, done; batches of
-//      independent loads) and compute delta_t = r_t + gamma V_{t+1} (1 - d_t) - V_t into LDS;
-//   2. one lane per env runs A_t = delta_t + c_t A_{t+1} out of LDS, c_t = (gamma lambda)(1 - d_t)
-//      selected from the done byte (one multiply and one add on the chain; operands read 8 steps
-//      ahead);
+//      independent loads) and write delta_t = r_t + gamma V_{t+1} (1 - d_t) - V_t and the chain
+//      coefficient c_t = (gamma lambda)(1 - d_t) (selected from the done byte) into env-major LDS
+//      rows, zero-padded to a multiple of 8 steps;
+//   2. one lane per env runs A_t = delta_t + c_t A_{t+1} down its rows, 8 steps per chunk, the
+//      next chunk's operands read as four 16-byte loads while this one's chain runs (one multiply
+//      and one add per step on the chain);
 //   3. all 256 threads write adv / ret back coalesced and accumulate the moments.
+// The padded steps run first, on zeros: A stays +0, which the chain starts from anyway.
+// Round 5: the chain read its operands as 16 scalar loads (delta, done byte) per 8 steps from
+// time-major rows and selected c_t on it: 11.7 of the phase's 23.7 us (DXRL_GAE_DIAG ablation,
+// profiles/r05/ab_gae_phases.log).
 // k_gae (64 single-wave workgroups, the whole step on the chain, a memory latency per 32-step
 // chunk) remains for horizons whose staging exceeds the LDS.
 #ifndef DXRL_GAE_XCD
 #define DXRL_GAE_XCD 1
+#endif
+// ablation bits for phase timing (A/B builds only; results are wrong when set): 1 no recurrence,
+// 2 no moments / merge, 4 no stores of adv / ret
+#ifndef DXRL_GAE_DIAG
+#define DXRL_GAE_DIAG 0
 #endif
 constexpr int kGlEnvs = 16, kGlThreads = 256;
 // Workgroups are dispatched to the 8 XCDs round robin (block b on XCD b % 8): env group g of
@@ -1145,22 +1156,30 @@ __device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t nb) {
     const int64_t q = nb / 8, rem = nb % 8, x = b % 8, j = b / 8;
     return x * q + (x < rem ? x : rem) + j;
 }
-__host__ __device__ constexpr int64_t gae_lds_bytes(int64_t T) { return T * kGlEnvs * 13; }
+// env-major row pitch (floats) of the delta / coefficient rows: the horizon padded to 8 steps,
+// + 4 so the 16 lanes' 16-byte reads start on distinct bank quads (T = 200: pitch 204)
+__host__ __device__ constexpr int64_t gae_pitch(int64_t T) { return (T + 7) / 8 * 8 + 4; }
+// delta + coefficient rows [16][pitch], V_t [T][16], A_t [T8][16] (the padded steps' A land past T)
+__host__ __device__ constexpr int64_t gae_lds_bytes(int64_t T) {
+    return kGlEnvs * (8 * gae_pitch(T) + 4 * T + 4 * ((T + 7) / 8 * 8));
+}
 __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict__ rew,
                                                         const uint8_t* __restrict__ done, const float* __restrict__ V,
                                                         int64_t n, int T, float gamma, float lam,
                                                         float* __restrict__ adv, float* __restrict__ ret,
                                                         Moments* __restrict__ partial) {
     extern __shared__ __attribute__((aligned(16))) float gl_lds[];
-    float* Ls = gl_lds;                           // [T][16] delta_t
-    float* Vs = Ls + (int64_t)T * kGlEnvs;         // [T][16] V_t (for ret)
-    float* As = Vs + (int64_t)T * kGlEnvs;         // [T][16] advantages
-    uint8_t* Ds = reinterpret_cast<uint8_t*>(As + (int64_t)T * kGlEnvs);  // [T][16] done
+    const int P = (int)gae_pitch(T), T8 = (T + 7) / 8 * 8;
+    float* Le = gl_lds;                            // [16][P] delta_t (env-major, zero past T)
+    float* Ce = Le + kGlEnvs * P;                  // [16][P] c_t
+    float* Vs = Ce + kGlEnvs * P;                  // [T][16] V_t (for ret)
+    float* As = Vs + (int64_t)T * kGlEnvs;         // [T8][16] advantages (rows T.. unused)
     __shared__ Moments red[kGlThreads];
     const int tid = threadIdx.x;
     const int64_t grp = DXRL_GAE_XCD ? xcd_contiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
     const int64_t e0 = grp * kGlEnvs;
     const int64_t cnt = (int64_t)T * kGlEnvs;
+    const float gl = gamma * lam;
     // 1. batches of kGlBatch elements per thread, every load issued before any lands
     constexpr int kGlBatch = 16;
     for (int64_t q0 = 0; q0 < cnt; q0 += (int64_t)kGlBatch * kGlThreads) {
@@ -1181,52 +1200,45 @@ __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict_
         for (int u = 0; u < kGlBatch; ++u) {
             const int64_t q = q0 + (int64_t)u * kGlThreads + tid;
             if (q < cnt) {
+                const int t = (int)(q / kGlEnvs), e = (int)(q % kGlEnvs);
                 const float nd = dv[u] ? 0.0f : 1.0f;
-                Ls[q] = rv[u] + gamma * v1[u] * nd - v0[u];
+                Le[e * P + t] = rv[u] + gamma * v1[u] * nd - v0[u];
+                Ce[e * P + t] = dv[u] ? 0.0f : gl;  // (gamma lambda) (1 - d_t), exactly
                 Vs[q] = v0[u];
-                Ds[q] = dv[u];
             }
         }
     }
+    for (int k = tid; k < kGlEnvs * (T8 - T); k += kGlThreads) {  // padded steps: zeros
+        const int e = k / (T8 - T), t = T + k % (T8 - T);
+        Le[e * P + t] = 0.0f;
+        Ce[e * P + t] = 0.0f;
+    }
     __syncthreads();
-    // 2. the recurrence
-    if (tid < kGlEnvs) {
+    // 2. the recurrence: lane e walks its rows down, chunk k = steps 8k .. 8k + 7
+    if (!(DXRL_GAE_DIAG & 1) && tid < kGlEnvs) {
         const int e = tid;
-        const float gl = gamma * lam;
+        const float4* L4 = reinterpret_cast<const float4*>(Le + e * P);
+        const float4* C4 = reinterpret_cast<const float4*>(Ce + e * P);
         float next_adv = 0.0f;
-        // chunks of kAh steps: the next chunk's operands are read while this one's chain runs
-        // (one LDS wait per chunk); steps past t = 0 in the last chunk run on clamped operands and
-        // are not stored
-        constexpr int kAh = 8;
-        float lq[kAh];
-        uint8_t dq[kAh];
+        int k = T8 / 8 - 1;
+        float4 l0 = L4[2 * k], l1 = L4[2 * k + 1], c0 = C4[2 * k], c1 = C4[2 * k + 1];
+        for (; k >= 0; --k) {
+            const int kn = k > 0 ? k - 1 : 0;  // the next chunk's operands (a reload of chunk 0 at the end)
+            const float4 nl0 = L4[2 * kn], nl1 = L4[2 * kn + 1], nc0 = C4[2 * kn], nc1 = C4[2 * kn + 1];
+            __builtin_amdgcn_sched_barrier(0);  // the loads stay ahead of the chain (the scheduler sank them)
+            const float lq[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+            const float cq[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
-        for (int j = 0; j < kAh; ++j) {
-            const int t = T - 1 - j >= 0 ? T - 1 - j : 0;
-            lq[j] = Ls[t * kGlEnvs + e];
-            dq[j] = Ds[t * kGlEnvs + e];
-        }
-        for (int t0 = T - 1; t0 >= 0; t0 -= kAh) {
-            float ln[kAh];
-            uint8_t dn[kAh];
-#pragma unroll
-            for (int j = 0; j < kAh; ++j) {
-                const int t = t0 - kAh - j >= 0 ? t0 - kAh - j : 0;
-                ln[j] = Ls[t * kGlEnvs + e];
-                dn[j] = Ds[t * kGlEnvs + e];
-            }
-#pragma unroll
-            for (int j = 0; j < kAh; ++j) {
-                const float c = dq[j] ? 0.0f : gl;  // (gamma lambda) (1 - d_t), exactly
-                const float a = lq[j] + c * next_adv;
-                if (t0 - j >= 0) As[(t0 - j) * kGlEnvs + e] = a;
+            for (int j = 7; j >= 0; --j) {
+                const float a = lq[j] + cq[j] * next_adv;
+                As[(8 * k + j) * kGlEnvs + e] = a;  // no branch: padded steps land in rows T .. T8 - 1
                 next_adv = a;
             }
-#pragma unroll
-            for (int j = 0; j < kAh; ++j) {
-                lq[j] = ln[j];
-                dq[j] = dn[j];
-            }
+            __builtin_amdgcn_sched_barrier(0);
+            l0 = nl0;
+            l1 = nl1;
+            c0 = nc0;
+            c1 = nc1;
         }
     }
     __syncthreads();
@@ -1237,8 +1249,11 @@ __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict_
         const int64_t t = q / kGlEnvs, e = q % kGlEnvs;
         if (e0 + e < n) {
             const float a = As[q];
-            adv[t * n + e0 + e] = a;
-            ret[t * n + e0 + e] = a + Vs[q];
+            if (!(DXRL_GAE_DIAG & 4)) {
+                adv[t * n + e0 + e] = a;
+                ret[t * n + e0 + e] = a + Vs[q];
+            }
+            if (DXRL_GAE_DIAG & 2) continue;
             if (c == 0.0) K = (double)a;
             const double d = (double)a - K;
             s += d;
@@ -1247,6 +1262,10 @@ __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict_
         }
     }
     const Moments mo = c > 0.0 ? Moments{c, K + s / c, fmax(s2 - s * (s / c), 0.0)} : Moments{0.0, 0.0, 0.0};
+    if (DXRL_GAE_DIAG & 2) {
+        if (tid == 0) partial[grp] = mo;
+        return;
+    }
     block_merge<kGlThreads>(mo, red);
     if (tid == 0) partial[grp] = red[0];
 }

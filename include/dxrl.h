@@ -310,9 +310,10 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
  * in a fixed order: no sum(a^2) - mean sum(a) cancellation).
  * The scan is the SEQUENTIAL recurrence A_t = delta_t + (gamma lambda)(1 - d_t) A_{t+1} per env,
  * bit-exact against a one-env-at-a-time reverse loop in that operation order:
- *   horizon * 208 B <= 152 KiB (T <= 748): k_gae_lds -- a 256-thread workgroup per 16 envs
- *     stages the horizon in LDS with all its threads (delta_t computed in parallel), one lane per
- *     env runs the two-op chain, all threads store adv / ret;  ceil(N / 16) workgroups;
+ *   T <= 600 (~256 B per step in LDS, <= 152 KiB): k_gae_lds -- a 256-thread workgroup per 16
+ *     envs stages the horizon in LDS with all its threads (delta_t and the chain coefficient
+ *     computed in parallel), one lane per env runs the two-op chain, all threads store adv / ret;
+ *     ceil(N / 16) workgroups;
  *   longer horizons: k_gae -- one thread per env, 64-env workgroups;  ceil(N / 64) workgroups.
  * Each workgroup writes one (count, mean, M2) triple into `partial`.
  * partial: f64 [dxrl_pg_gae_partial_doubles(N, T)] (= 3 ceil(N / 16), enough for either kernel);

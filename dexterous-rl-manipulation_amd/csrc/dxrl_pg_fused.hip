@@ -408,6 +408,11 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #define DXRL_FUSED_PRIO 1
 #endif
 
+// forward-only pass with resident weights: the next tile's X fetched at the start of the tile
+#ifndef DXRL_FWD_EARLY_X
+#define DXRL_FWD_EARLY_X 1
+#endif
+
 // kFW waves per workgroup: 4 (one per SIMD, 512 registers each) or 8 (two per SIMD)
 // kTrain: forward + heads + backward; otherwise the forward-only critic-value pass, which keeps
 // no launch-long accumulators and so fits two waves per SIMD.
@@ -505,6 +510,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     // whole launch (80 VGPRs; the train instantiations have no room for them) instead of streaming
     // 160 KB of weight fragments from L2 per tile and workgroup
     constexpr bool kResW = !kTrain && kNT == 1 && DXRL_FWD_RESIDENT_W && DXRL_L2_PIPE;
+    constexpr bool kEarlyX = kResW && DXRL_FWD_EARLY_X;
     bf16x8 w1res[kResW ? kIn / 16 : 1], w2res[kResW ? kH / 16 : 1];
     if constexpr (kResW) {
         const gbf16x8* p1 = (const gbf16x8*)p.W1 + (int64_t)ft0 * (kIn / 16) * 64 + lane;
@@ -565,6 +571,12 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         for (int u = 0; u < kXU; ++u) {
             const int c = tid + kFThreads * u, row = c >> 3, col = 8 * (c & 7);
             *reinterpret_cast<bf16x8*>(X + row * kXp + col) = xr[u];
+        }
+        // resident-weight forward pass: no weight fragment loads in the tile loop, so nothing
+        // waits behind the next tile's X -- it goes out now and lands under this tile's layers
+        // (fetched after the head it was a full HBM latency at the next tile's start)
+        if constexpr (kEarlyX) {
+            if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
         }
         // the first W1 fragments go out before the barrier (their L2 latency overlaps its wait;
         // issued after the X stores, so they do not queue behind the X tile's HBM loads)
@@ -939,7 +951,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         }
         STAMP(6);
         if (!kTrain) {
-            if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
+            if (!kEarlyX && tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
             __syncthreads();  // X / H1 / H2 are rewritten by the next tile
             STAMP(7);
             continue;

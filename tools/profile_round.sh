@@ -36,7 +36,7 @@ if [ -z "${SKIP_PMC:-}" ]; then
   step pmc_sq 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/pmc_sq -o run -- python3 tools/prof_pg_iter.py
   python tools/pmc_kernels.py "$O/pmc_sq/**/*counter_collection.csv" > $O/pmc_sq.json
 fi
-CFGS=${CFGS:-easy default hard_heldout variable_noise}
+CFGS=${CFGS-easy default hard_heldout variable_noise}  # CFGS="" skips the per-config lines
 for c in $CFGS; do
   if [ "$c" = easy ]; then step bench_$c 300 python bench.py; else
     step bench_$c 200 python bench.py --config $c --no-cpu-baseline --no-roofline; fi

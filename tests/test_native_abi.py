@@ -71,6 +71,25 @@ def test_gae_partial_size_query(native):
         native.gae_partial_doubles(0, 5)
 
 
+def test_gnorm_partials_query_and_argument_checks(native):
+    """dxrl_pg_gnorm_blocks: one f64 partial per block of the paired reduction (both networks'
+    fused-pass slab blocks and dW2 blocks: 2 x (ceil(16,720 / 4 / 16) + 256 x 256 / 64) = 2,572);
+    dxrl_pg_fused_pair_gnorm / dxrl_pg_adam_step reject bad arguments before touching a device."""
+    nb = C.c_int32()
+    native.call("dxrl_pg_gnorm_blocks", C.byref(nb))
+    assert nb.value == 2 * ((16720 // 4 + 15) // 16 + 256 * 256 // 64) == 2572
+    a, c = native.PgFusedArgs(), native.PgFusedArgs()
+    with pytest.raises(ValueError, match="gnorm_blocks"):
+        native.call("dxrl_pg_fused_pair_gnorm", 0, C.byref(c), C.byref(a), 4096, 2572, None, None)
+    fake = 1 << 20  # never dereferenced: the checks run first
+    with pytest.raises(ValueError, match="padded parameter count"):
+        native.call("dxrl_pg_adam_step", 0, *([fake] * 7), 12345, 3e-4, 0.9, 0.999, 1e-5, 1, 0.5, fake, 2572, fake,
+                    fake, None)
+    with pytest.raises(ValueError, match="adam_step"):
+        native.call("dxrl_pg_adam_step", 0, *([fake] * 7), 12345, 3e-4, 0.9, 0.999, 1e-5, 1, 0.5, fake, 0, fake,
+                    fake, None)
+
+
 STRUCTS = ["dxrl_curriculum", "dxrl_env_config", "dxrl_env_layout", "dxrl_learner_layout", "dxrl_learner_config",
            "dxrl_rollout_io", "dxrl_pg_rollout_args", "dxrl_pg_heads_args",
            "dxrl_pg_fused_args", "dxrl_eval_segment", "dxrl_eval_args", "dxrl_sched_args", "dxrl_sched_packed_args"]

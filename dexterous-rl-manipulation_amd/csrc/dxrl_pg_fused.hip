@@ -271,6 +271,61 @@ struct EpiGate {
     }
 };
 
+// Forward-only pass, both layers software-pipelined across sample tiles (resident W1 / W2, one
+// 32-feature tile per wave).  Stage s = 0 .. MT: L1's chain for sample tile s, then L2's chain for
+// tile s - 1 with, in its MFMA gaps, the tanh epilogues of L2(s - 2) (k-steps 0..7) and of L1(s)
+// (k-steps 8..15); a barrier closes each stage (H1 rows of tile s complete before any wave's
+// L2(s) reads them).  Two waves of a SIMD then never sit in an MFMA-only or VALU-only phase except
+// at the two ends, where the lockstep layer-by-layer form had one of each per layer.  Every output
+// is the same MFMA chain in the same k order and the same epilogue as fwd_pipe_w's, so H1 / H2
+// (and V) are bit for bit the layer-by-layer pass's.
+template <int KS1, int KS2, int MT>
+__device__ __forceinline__ void fwd_xlayer(const bf16x8 (&w1)[KS1], const bf16x8 (&w2)[KS2], const bf16* X, bf16* H1,
+                                           bf16* H2, int lane, int f0, const float* bk2) {
+    static_assert(KS2 == 16, "8 + 8 epilogue pairs over L2's 16 k-steps");
+    const int r = lane & 31, h = lane >> 5;
+    EpiTanh e1{H1, f0, r, nullptr};
+    EpiTanh e2{H2, f0, r, bk2};
+    const bf16* xp = X + r * kXp + 8 * h;
+    const bf16* hp = H1 + r * kHp + 8 * h;
+    f32x16 a1, a2, p2;  // L1(s), L2(s - 1), L2(s - 2)
+    constexpr int kBD = 3;
+#pragma unroll
+    for (int s = 0; s <= MT; ++s) {
+        if (s < MT) {
+            bf16x8 b[KS1];
+#pragma unroll
+            for (int k = 0; k < KS1; ++k) b[k] = *reinterpret_cast<const bf16x8*>(xp + 32 * s * kXp + 16 * k);
+            zero_acc(a1);
+#pragma unroll
+            for (int k = 0; k < KS1; ++k) a1 = mfma32(w1[k], b[k], a1);
+        }
+        if (s == 0) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) e1(a1, 0, q);
+        } else {
+            const bf16* ap = hp + 32 * (s - 1) * kHp;
+            bf16x8 bq[kBD + 1];
+#pragma unroll
+            for (int i = 0; i < kBD; ++i) bq[i] = *reinterpret_cast<const bf16x8*>(ap + 16 * i);
+            zero_acc(a2);
+#pragma unroll
+            for (int k = 0; k < KS2; ++k) {
+                if (k + kBD < KS2) bq[(k + kBD) % (kBD + 1)] = *reinterpret_cast<const bf16x8*>(ap + 16 * (k + kBD));
+                __builtin_amdgcn_sched_barrier(0);
+                a2 = mfma32(w2[k], bq[k % (kBD + 1)], a2);
+                if (k < 8 && s >= 2) e2(p2, s - 2, k);
+                if (k >= 8 && s < MT) e1(a1, s, k - 8);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            p2 = a2;
+        }
+        if (s < MT) __syncthreads();  // (after the last stage the head's barrier follows the tail)
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) e2(p2, MT - 1, q);
+}
+
 // tanh(acc + bias) -> bf16 row-major activation tile (4 consecutive features per 8-byte store)
 // (bk: the lane's 16 pre-scaled biases tanh_bias(b[32 ft + 8 g + 4 h + u]) at [4 g + u], or null)
 template <int MT>
@@ -412,6 +467,12 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #ifndef DXRL_FWD_EARLY_X
 #define DXRL_FWD_EARLY_X 1
 #endif
+// forward-only pass with resident weights: L1 / L2 pipelined across sample tiles (fwd_xlayer);
+// measured 3 % slower than layer by layer (158.5 vs 154 us, bit-identical: four more barriers
+// per tile cost more than the overlap wins; profiles/r05/ab_fwd_xlayer_rejected.log) -- off
+#ifndef DXRL_FWD_XLAYER
+#define DXRL_FWD_XLAYER 0
+#endif
 
 // kFW waves per workgroup: 4 (one per SIMD, 512 registers each) or 8 (two per SIMD)
 // kTrain: forward + heads + backward; otherwise the forward-only critic-value pass, which keeps
@@ -511,6 +572,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     // 160 KB of weight fragments from L2 per tile and workgroup
     constexpr bool kResW = !kTrain && kNT == 1 && DXRL_FWD_RESIDENT_W && DXRL_L2_PIPE;
     constexpr bool kEarlyX = kResW && DXRL_FWD_EARLY_X;
+    constexpr bool kXL = kResW && DXRL_FWD_XLAYER;  // both layers pipelined across sample tiles
     bf16x8 w1res[kResW ? kIn / 16 : 1], w2res[kResW ? kH / 16 : 1];
     if constexpr (kResW) {
         const gbf16x8* p1 = (const gbf16x8*)p.W1 + (int64_t)ft0 * (kIn / 16) * 64 + lane;
@@ -594,18 +656,22 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // HBM load issued here would make every weight-fragment wait below wait for it too)
 
         // ---- L1, L2 (wave w: hidden features 64w .. 64w + 63, all 128 samples)
+        if constexpr (kXL) {
+            fwd_xlayer<kIn / 16, kH / 16, kMT>(w1res, w2res, X, H1, H2, lane, 32 * ft0 + 4 * h, bkres);
+        } else {
 #pragma unroll 1
-        for (int j = 0; j < kNT; ++j) {
-            // bias = W1 column 45 (X column 45 = 1)
-            if (j > 0) w_prefetch(pw1, W1, kIn / 16, ft0 + j, lane);
-            EpiTanh e1{H1, 32 * (ft0 + j) + 4 * h, r, nullptr};
-            fwd_pipe<kIn / 16, kXp, kMT>(pw1, X, lane, e1);
+            for (int j = 0; j < kNT; ++j) {
+                // bias = W1 column 45 (X column 45 = 1)
+                if (j > 0) w_prefetch(pw1, W1, kIn / 16, ft0 + j, lane);
+                EpiTanh e1{H1, 32 * (ft0 + j) + 4 * h, r, nullptr};
+                fwd_pipe<kIn / 16, kXp, kMT>(pw1, X, lane, e1);
+            }
         }
         // the first W2 fragments go out before the barrier (their L2 latency overlaps its wait)
         WPre<kH / 16> pw2;
         if constexpr (!kResW) w_prefetch(pw2, W2, kH / 16, ft0, lane);
         STAMP(2);
-        __syncthreads();
+        if constexpr (!kXL) __syncthreads();
         STAMP(3);
         // head inputs (HBM), issued halfway through L2 so their latency hides behind its second half
         const int ml = 32 * wave + r;
@@ -649,7 +715,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             }
         };
 #pragma unroll 1
-        for (int j = 0; j < kNT; ++j) {
+        for (int j = 0; j < (kXL ? 0 : kNT); ++j) {
             bft = ft0 + j;
             const auto l2_hook = [&]() {
                 if (j == kNT - 1) head_inputs();

@@ -1516,6 +1516,10 @@ int dxrl_pg_fused_pair_gnorm(int32_t device, const dxrl_pg_fused_args* c, const 
                              double* gnorm_partial, int32_t gnorm_capacity, int32_t* gnorm_blocks, void* stream) {
     DXRL_REQUIRE(c && a, "fused_pair: null arguments");
     DXRL_REQUIRE(!gnorm_partial || gnorm_blocks, "fused_pair: gnorm_partial needs gnorm_blocks");
+    const int nb1 = (int)((kPartSize / 4 + 15) / 16), nb2 = kH * kH / 4 / 16;  // reduction blocks per network
+    // (checked before anything is launched: a failed call leaves the gradient untouched)
+    DXRL_REQUIRE(!gnorm_partial || gnorm_capacity >= 2 * (nb1 + nb2), "fused_pair: gnorm_partial needs %d doubles",
+                 2 * (nb1 + nb2));
     DXRL_REQUIRE(c->net == 1 && a->net == 0 && c->train && a->train, "fused_pair: a critic and an actor train pass");
     DXRL_REQUIRE(c->rows == a->rows && c->rows > 0 && c->rows % 32 == 0 && c->obs == a->obs && c->packed == a->packed &&
                      c->grads == a->grads && c->params == a->params,
@@ -1552,11 +1556,7 @@ int dxrl_pg_fused_pair_gnorm(int32_t device, const dxrl_pg_fused_args* c, const 
                                       kHx, st, &ns_c, &ns_a))
         return rc;
     DXRL_REQUIRE(ns_c > kReduceGroups && ns_a > kReduceGroups, "fused_pair: too few rows for the splits");
-    const int nb1 = (int)((kPartSize / 4 + 15) / 16), nb2 = kH * kH / 4 / 16;
-    if (gnorm_partial) {
-        DXRL_REQUIRE(gnorm_capacity >= 2 * (nb1 + nb2), "fused_pair: gnorm_partial needs %d doubles", 2 * (nb1 + nb2));
-        *gnorm_blocks = 2 * (nb1 + nb2);
-    }
+    if (gnorm_partial) *gnorm_blocks = 2 * (nb1 + nb2);
     GradReduceNet rc_{reinterpret_cast<const float4*>(c->partial), grid_c, G + kOffW1c, G + kOffW3c, nullptr,
                       G + kOffW2c, (float)c->ent_coef, reinterpret_cast<const float4*>(c->wgrad_partial), ns_c,
                       (int64_t)kHx, nb1, nb2};

@@ -81,6 +81,8 @@ def test_gnorm_partials_query_and_argument_checks(native):
     a, c = native.PgFusedArgs(), native.PgFusedArgs()
     with pytest.raises(ValueError, match="gnorm_blocks"):
         native.call("dxrl_pg_fused_pair_gnorm", 0, C.byref(c), C.byref(a), 4096, 2572, None, None)
+    with pytest.raises(ValueError, match="2572 doubles"):  # checked before any launch
+        native.call("dxrl_pg_fused_pair_gnorm", 0, C.byref(c), C.byref(a), 4096, 2571, C.byref(nb), None)
     fake = 1 << 20  # never dereferenced: the checks run first
     with pytest.raises(ValueError, match="padded parameter count"):
         native.call("dxrl_pg_adam_step", 0, *([fake] * 7), 12345, 3e-4, 0.9, 0.999, 1e-5, 1, 0.5, fake, 2572, fake,

@@ -1307,6 +1307,95 @@ __device__ __forceinline__ double sumsq4(float a, float b, float c, float d) {
     return (((double)a * a + (double)b * b) + (double)c * c) + (double)d * d;
 }
 
+// Critic values (the forward-only pass) as its own kernel, pipelined across tiles: the layer-by-layer
+// instantiation k_pg_fused<8, 128, false, 1> closes four barriers per tile (X stored, L1 -> L2,
+// L2 -> head, end of tile).  Here the next tile's X is stored while L2 runs (X is free once L1 is
+// done) and the next tile's L1 runs beside this tile's value head (H1 is free once L2 is done, H2
+// is not written again until the next L2): two barriers per tile.  Same resident W1 / W2 / biases /
+// value row, same fwd_pipe_w chains, epilogues and 16x16x32 head as the layer-by-layer pass, so V
+// is bit for bit its V (test_values_kernel_equals_layer_by_layer_pass).
+#ifndef DXRL_FWD_VALUES
+#define DXRL_FWD_VALUES 1
+#endif
+__global__ __launch_bounds__(512, 1) void k_pg_values(FusedArgs p) {
+    using L = TileLds<128>;
+    constexpr int kMT = 4, kXU = 128 * (kIn / 8) / 512;
+    __shared__ __attribute__((aligned(16))) bf16 lds[L::kElems];
+    bf16* X = lds + L::kOffX;
+    bf16* H1 = lds + L::kOffH1;
+    bf16* H2 = lds + L::kOffH2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+#if DXRL_FUSED_PRIO
+    if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+    const int64_t ntiles = (p.rows + 127) / 128;
+    int64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;  // (the launch clamps the grid to the tile count)
+    bf16x8 xr[kXU];
+    const auto fetch_x = [&](int64_t t) {
+#pragma unroll
+        for (int u = 0; u < kXU; ++u) {
+            const int c = tid + 512 * u, row = c >> 3, col = 8 * (c & 7);
+            const int64_t m = t * 128 + row;
+            xr[u] = m < p.rows ? *reinterpret_cast<const bf16x8*>(p.X + m * kIn + col) : zero8();
+        }
+    };
+    const auto store_x = [&]() {
+#pragma unroll
+        for (int u = 0; u < kXU; ++u) {
+            const int c = tid + 512 * u, row = c >> 3, col = 8 * (c & 7);
+            *reinterpret_cast<bf16x8*>(X + row * kXp + col) = xr[u];
+        }
+    };
+    fetch_x(tile);
+    // this wave's 32 hidden units: W1 / W2 fragments, layer-2 biases, the value row (resident)
+    bf16x8 w1[kIn / 16], w2[kH / 16], w3h[8];
+    {
+        const gbf16x8* p1 = (const gbf16x8*)p.W1 + (int64_t)wave * (kIn / 16) * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < kIn / 16; ++k) w1[k] = p1[64 * k];
+        const gbf16x8* p2 = (const gbf16x8*)p.W2 + (int64_t)wave * (kH / 16) * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < kH / 16; ++k) w2[k] = p2[64 * k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            w3h[k] = (lane & 15) == 0 ? *(const gbf16x8*)(p.W3rm + 32 * k + 8 * (lane >> 4)) : zero8();
+    }
+    float bk[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) bk[q] = tanh_bias(((gf32*)p.b2)[(int64_t)(32 * wave + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
+    const float b3h = ((gf32*)p.b3)[0];
+    EpiTanh e1{H1, 32 * wave + 4 * h, r, nullptr};
+    EpiTanh e2{H2, 32 * wave + 4 * h, r, bk};
+    store_x();
+    if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
+    __syncthreads();
+    fwd_pipe_w<kIn / 16, kXp, kMT>(w1, X, lane, e1);
+    __syncthreads();  // H1 of the first tile complete, X free
+    for (;;) {
+        const int64_t next = tile + gridDim.x;
+        fwd_pipe_w<kH / 16, kHp, kMT>(w2, H1, lane, e2);
+        if (next < ntiles) {
+            store_x();  // X(next): every wave finished L1(tile) before the last barrier
+            if (next + gridDim.x < ntiles) fetch_x(next + gridDim.x);
+        }
+        __syncthreads();  // H2(tile) and X(next) complete; H1 free
+        {  // value head: wave w, samples 16 w .. + 15; V of sample 16 w + l in lane l < 16
+            const int s16 = 16 * wave + (lane & 15);
+            const bf16* hb = H2 + s16 * kHp + 8 * (lane >> 4);
+            f32x4 a16 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a16 = mfma16(w3h[k], *reinterpret_cast<const bf16x8*>(hb + 32 * k), a16);
+            const int64_t m16 = tile * 128 + s16;
+            if (m16 < p.rows && lane < 16) p.v_out[m16] = a16[0] + b3h;
+        }
+        if (next >= ntiles) break;
+        fwd_pipe_w<kIn / 16, kXp, kMT>(w1, X, lane, e1);  // L1(next) beside the other waves' heads
+        __syncthreads();  // H1(next) complete; H2 and X free
+        tile = next;
+    }
+}
+
 // The workgroup partials summed and scattered in one launch: a 256-thread block owns 16 float4
 // columns of the [z][kPartSize] slabs; with z > kReduceGroups thread (g, x) sums group g's slabs
 // of column x in order and the 16 group sums are added in group order (launch_slab_reduce's two
@@ -1647,7 +1736,11 @@ int fused_kernel(const dxrl_pg_fused_args* a, hipStream_t st, int* grid_out) {
         else if (!c) hipLaunchKernelGGL((k_pg_fused<4, 64, true, 0, true>), dim3(grid), dim3(256), 0, st, f);
         else hipLaunchKernelGGL((k_pg_fused<4, 64, true, 1, true>), dim3(grid), dim3(256), 0, st, f);
     } else if (!train) {
+        // A/B and the bit-identity test: the layer-by-layer instantiation (DXRL_FWD_LAYERED=1, read per call)
+        const char* lv = getenv("DXRL_FWD_LAYERED");
+        const bool layered = lv && atoi(lv) != 0;
         if (dg) hipLaunchKernelGGL((k_pg_fused<8, 128, false, 1, true>), dim3(grid), dim3(512), 0, st, f);
+        else if (DXRL_FWD_VALUES && !layered) hipLaunchKernelGGL(k_pg_values, dim3(grid), dim3(512), 0, st, f);
         else hipLaunchKernelGGL((k_pg_fused<8, 128, false, 1, false>), dim3(grid), dim3(512), 0, st, f);
     } else if (!c) {
         if (dg) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 0, true>), dim3(grid), dim3(512), 0, st, f);

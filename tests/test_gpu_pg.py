@@ -278,6 +278,24 @@ def test_reduction_gnorm_partials_match_sumsq_path(pkg, n, T, mb, max_norm):
         assert not any(engaged), engaged
 
 
+@pytest.mark.parametrize("n,T", [(773, 32), (4096, 200), (96, 1)])
+def test_values_kernel_equals_layer_by_layer_pass(pkg, n, T, monkeypatch):
+    """The critic-values kernel pipelined across tiles (k_pg_values: next X stored under L2, next L1
+    beside the value head) == the layer-by-layer forward instantiation bit for bit, at a ragged
+    row count (773 x 33 rows), the full bench shape and a single tile per workgroup."""
+    _, tr = make(pkg, n, T)
+    tr.rollout()
+    tr.critic_values()
+    torch.cuda.synchronize()
+    v_pipe = tr.V.clone()
+    tr.V.fill_(float("nan"))
+    monkeypatch.setenv("DXRL_FWD_LAYERED", "1")
+    tr.critic_values()
+    torch.cuda.synchronize()
+    assert torch.equal(tr.V, v_pipe)
+    assert torch.isfinite(v_pipe[0, :(T + 1) * n]).all()
+
+
 def test_adam_matches_manual(pkg):
     env, tr = make(pkg, 64, 16)
     tr.grads.normal_(0, 1e-3)

@@ -252,6 +252,23 @@ struct EpiTanh {
         if (u == 2) *reinterpret_cast<bf16x4*>(H + (32 * mt + r) * kHp + f0 + 8 * g) = v;
     }
 };
+// EpiTanh with the 16 pre-scaled biases held by value (k_pg_values: through a pointer the
+// run-time tile-count dispatch kept them in scratch memory)
+struct EpiTanhB {
+    bf16* H;
+    int f0;
+    int r;
+    float bk[16];
+    bf16x4 v;
+    __device__ void prime(int) {}
+    __device__ __forceinline__ void operator()(const f32x16& acc, int mt, int p) {
+        const int g = p >> 1, u = 2 * (p & 1);
+        const f32x2 t = tanh_pre2(f32x2{acc[4 * g + u], acc[4 * g + u + 1]}, f32x2{bk[4 * g + u], bk[4 * g + u + 1]});
+        v[u] = to_bf16(t.x);
+        v[u + 1] = to_bf16(t.y);
+        if (u == 2) *reinterpret_cast<bf16x4*>(H + (32 * mt + r) * kHp + f0 + 8 * g) = v;
+    }
+};
 struct EpiGate {
     bf16* Y;
     int f0;
@@ -1311,15 +1328,29 @@ __device__ __forceinline__ double sumsq4(float a, float b, float c, float d) {
 // instantiation k_pg_fused<8, 128, false, 1> closes four barriers per tile (X stored, L1 -> L2,
 // L2 -> head, end of tile).  Here the next tile's X is stored while L2 runs (X is free once L1 is
 // done) and the next tile's L1 runs beside this tile's value head (H1 is free once L2 is done, H2
-// is not written again until the next L2): two barriers per tile.  Same resident W1 / W2 / biases /
-// value row, same fwd_pipe_w chains, epilogues and 16x16x32 head as the layer-by-layer pass, so V
-// is bit for bit its V (test_values_kernel_equals_layer_by_layer_pass).
+// is not written again until the next L2): two barriers per tile.  Rows: every workgroup runs the
+// same number of whole 128-row tiles, then one share of the remaining rows (< 128 per workgroup,
+// ceil(remainder / grid) each) as a short tile of 1-4 32-row MFMA tiles -- at the bench shape the
+// T + 1 observation blocks are 25 tiles and 16 rows per workgroup, where the layer-by-layer grid
+// ran a 26th round of whole tiles on 32 workgroups.  Same resident W1 / W2 / biases / value row,
+// same fwd_pipe_w chains, epilogues and 16x16x32 head as the layer-by-layer pass, and a row's V
+// depends only on its own observation row, so V is bit for bit that pass's V
+// (test_values_kernel_equals_layer_by_layer_pass).
 #ifndef DXRL_FWD_VALUES
 #define DXRL_FWD_VALUES 1
 #endif
+template <int KS, int kLda, typename Epi>
+__device__ __forceinline__ void fwd_pipe_w_mt(int mt, const bf16x8 (&wf)[KS], const bf16* A, int lane, Epi& epi) {
+    switch (mt) {  // workgroup-uniform
+        case 1: fwd_pipe_w<KS, kLda, 1>(wf, A, lane, epi); break;
+        case 2: fwd_pipe_w<KS, kLda, 2>(wf, A, lane, epi); break;
+        case 3: fwd_pipe_w<KS, kLda, 3>(wf, A, lane, epi); break;
+        default: fwd_pipe_w<KS, kLda, 4>(wf, A, lane, epi); break;
+    }
+}
 __global__ __launch_bounds__(512, 1) void k_pg_values(FusedArgs p) {
     using L = TileLds<128>;
-    constexpr int kMT = 4, kXU = 128 * (kIn / 8) / 512;
+    constexpr int kXU = 128 * (kIn / 8) / 512;
     __shared__ __attribute__((aligned(16))) bf16 lds[L::kElems];
     bf16* X = lds + L::kOffX;
     bf16* H1 = lds + L::kOffH1;
@@ -1328,16 +1359,22 @@ __global__ __launch_bounds__(512, 1) void k_pg_values(FusedArgs p) {
 #if DXRL_FUSED_PRIO
     if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
-    const int64_t ntiles = (p.rows + 127) / 128;
-    int64_t tile = blockIdx.x;
-    if (tile >= ntiles) return;  // (the launch clamps the grid to the tile count)
+    // this workgroup's tiles: k < full -> rows (b + k G) 128 .. + 127; k == full -> its share of the rest
+    const int64_t G = gridDim.x, b = blockIdx.x;
+    const int64_t full = p.rows / 128 / G, main_rows = full * G * 128, rem = p.rows - main_rows;
+    const int64_t rper = (rem + G - 1) / G;  // <= 128 (rem < 128 G)
+    const int64_t r_lo = main_rows + b * rper, r_hi = min(p.rows, r_lo + rper);
+    const int64_t ntile = full + (r_hi > r_lo ? 1 : 0);
+    if (ntile == 0) return;  // workgroup-uniform
+    const auto row0 = [&](int64_t k) { return k < full ? (b + k * G) * 128 : r_lo; };
+    const auto count = [&](int64_t k) { return k < full ? (int64_t)128 : r_hi - r_lo; };
     bf16x8 xr[kXU];
-    const auto fetch_x = [&](int64_t t) {
+    const auto fetch_x = [&](int64_t k) {
+        const int64_t base = row0(k), cnt = count(k);
 #pragma unroll
         for (int u = 0; u < kXU; ++u) {
             const int c = tid + 512 * u, row = c >> 3, col = 8 * (c & 7);
-            const int64_t m = t * 128 + row;
-            xr[u] = m < p.rows ? *reinterpret_cast<const bf16x8*>(p.X + m * kIn + col) : zero8();
+            xr[u] = row < cnt ? *reinterpret_cast<const bf16x8*>(p.X + (base + row) * kIn + col) : zero8();
         }
     };
     const auto store_x = [&]() {
@@ -1347,52 +1384,56 @@ __global__ __launch_bounds__(512, 1) void k_pg_values(FusedArgs p) {
             *reinterpret_cast<bf16x8*>(X + row * kXp + col) = xr[u];
         }
     };
-    fetch_x(tile);
+    int64_t k = 0;
+    fetch_x(k);
     // this wave's 32 hidden units: W1 / W2 fragments, layer-2 biases, the value row (resident)
     bf16x8 w1[kIn / 16], w2[kH / 16], w3h[8];
     {
         const gbf16x8* p1 = (const gbf16x8*)p.W1 + (int64_t)wave * (kIn / 16) * 64 + lane;
 #pragma unroll
-        for (int k = 0; k < kIn / 16; ++k) w1[k] = p1[64 * k];
+        for (int q = 0; q < kIn / 16; ++q) w1[q] = p1[64 * q];
         const gbf16x8* p2 = (const gbf16x8*)p.W2 + (int64_t)wave * (kH / 16) * 64 + lane;
 #pragma unroll
-        for (int k = 0; k < kH / 16; ++k) w2[k] = p2[64 * k];
+        for (int q = 0; q < kH / 16; ++q) w2[q] = p2[64 * q];
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            w3h[k] = (lane & 15) == 0 ? *(const gbf16x8*)(p.W3rm + 32 * k + 8 * (lane >> 4)) : zero8();
+        for (int q = 0; q < 8; ++q)
+            w3h[q] = (lane & 15) == 0 ? *(const gbf16x8*)(p.W3rm + 32 * q + 8 * (lane >> 4)) : zero8();
     }
     float bk[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) bk[q] = tanh_bias(((gf32*)p.b2)[(int64_t)(32 * wave + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
     const float b3h = ((gf32*)p.b3)[0];
     EpiTanh e1{H1, 32 * wave + 4 * h, r, nullptr};
-    EpiTanh e2{H2, 32 * wave + 4 * h, r, bk};
+    EpiTanhB e2{H2, 32 * wave + 4 * h, r, {}, {}};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) e2.bk[q] = bk[q];
+    const auto mts = [&](int64_t kk) { return (int)((count(kk) + 31) / 32); };  // 32-row MFMA tiles
     store_x();
-    if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
+    if (k + 1 < ntile) fetch_x(k + 1);
     __syncthreads();
-    fwd_pipe_w<kIn / 16, kXp, kMT>(w1, X, lane, e1);
+    fwd_pipe_w_mt<kIn / 16, kXp>(mts(k), w1, X, lane, e1);
     __syncthreads();  // H1 of the first tile complete, X free
     for (;;) {
-        const int64_t next = tile + gridDim.x;
-        fwd_pipe_w<kH / 16, kHp, kMT>(w2, H1, lane, e2);
-        if (next < ntiles) {
-            store_x();  // X(next): every wave finished L1(tile) before the last barrier
-            if (next + gridDim.x < ntiles) fetch_x(next + gridDim.x);
+        fwd_pipe_w_mt<kH / 16, kHp>(mts(k), w2, H1, lane, e2);
+        if (k + 1 < ntile) {
+            store_x();  // X(k + 1): every wave finished L1(k) before the last barrier
+            if (k + 2 < ntile) fetch_x(k + 2);
         }
-        __syncthreads();  // H2(tile) and X(next) complete; H1 free
+        __syncthreads();  // H2(k) and X(k + 1) complete; H1 free
         {  // value head: wave w, samples 16 w .. + 15; V of sample 16 w + l in lane l < 16
             const int s16 = 16 * wave + (lane & 15);
-            const bf16* hb = H2 + s16 * kHp + 8 * (lane >> 4);
-            f32x4 a16 = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (s16 < 32 * mts(k)) {  // (rows past the tile's MFMA tiles were never computed)
+                const bf16* hb = H2 + s16 * kHp + 8 * (lane >> 4);
+                f32x4 a16 = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-            for (int k = 0; k < 8; ++k) a16 = mfma16(w3h[k], *reinterpret_cast<const bf16x8*>(hb + 32 * k), a16);
-            const int64_t m16 = tile * 128 + s16;
-            if (m16 < p.rows && lane < 16) p.v_out[m16] = a16[0] + b3h;
+                for (int q = 0; q < 8; ++q) a16 = mfma16(w3h[q], *reinterpret_cast<const bf16x8*>(hb + 32 * q), a16);
+                if (s16 < count(k) && lane < 16) p.v_out[row0(k) + s16] = a16[0] + b3h;
+            }
         }
-        if (next >= ntiles) break;
-        fwd_pipe_w<kIn / 16, kXp, kMT>(w1, X, lane, e1);  // L1(next) beside the other waves' heads
-        __syncthreads();  // H1(next) complete; H2 and X free
-        tile = next;
+        if (k + 1 >= ntile) break;
+        fwd_pipe_w_mt<kIn / 16, kXp>(mts(k + 1), w1, X, lane, e1);  // L1(k + 1) beside the other waves' heads
+        __syncthreads();  // H1(k + 1) complete; H2 and X free
+        ++k;
     }
 }
 

@@ -1339,6 +1339,9 @@ __device__ __forceinline__ double sumsq4(float a, float b, float c, float d) {
 #ifndef DXRL_FWD_VALUES
 #define DXRL_FWD_VALUES 1
 #endif
+#ifndef DXRL_VALUES_HEAD_SPLIT
+#define DXRL_VALUES_HEAD_SPLIT 1
+#endif
 template <int KS, int kLda, typename Epi>
 __device__ __forceinline__ void fwd_pipe_w_mt(int mt, const bf16x8 (&wf)[KS], const bf16* A, int lane, Epi& epi) {
     switch (mt) {  // workgroup-uniform
@@ -1420,7 +1423,7 @@ __global__ __launch_bounds__(512, 1) void k_pg_values(FusedArgs p) {
             if (k + 2 < ntile) fetch_x(k + 2);
         }
         __syncthreads();  // H2(k) and X(k + 1) complete; H1 free
-        {  // value head: wave w, samples 16 w .. + 15; V of sample 16 w + l in lane l < 16
+        const auto head = [&]() {  // value head: wave w, samples 16 w .. + 15; V of sample 16 w + l in lane l < 16
             const int s16 = 16 * wave + (lane & 15);
             if (s16 < 32 * mts(k)) {  // (rows past the tile's MFMA tiles were never computed)
                 const bf16* hb = H2 + s16 * kHp + 8 * (lane >> 4);
@@ -1429,9 +1432,20 @@ __global__ __launch_bounds__(512, 1) void k_pg_values(FusedArgs p) {
                 for (int q = 0; q < 8; ++q) a16 = mfma16(w3h[q], *reinterpret_cast<const bf16x8*>(hb + 32 * q), a16);
                 if (s16 < count(k) && lane < 16) p.v_out[row0(k) + s16] = a16[0] + b3h;
             }
+        };
+        if (k + 1 >= ntile) {
+            head();
+            break;
         }
-        if (k + 1 >= ntile) break;
-        fwd_pipe_w_mt<kIn / 16, kXp>(mts(k + 1), w1, X, lane, e1);  // L1(k + 1) beside the other waves' heads
+        // L1(k + 1) beside the heads: the two waves of a SIMD in opposite orders, so one's head MFMAs
+        // run beside the other's L1 epilogue (DXRL_VALUES_HEAD_SPLIT; 0: head first on every wave)
+        if (DXRL_VALUES_HEAD_SPLIT && __builtin_amdgcn_readfirstlane(wave) >= 4) {
+            fwd_pipe_w_mt<kIn / 16, kXp>(mts(k + 1), w1, X, lane, e1);
+            head();
+        } else {
+            head();
+            fwd_pipe_w_mt<kIn / 16, kXp>(mts(k + 1), w1, X, lane, e1);
+        }
         __syncthreads();  // H1(k + 1) complete; H2 and X free
         ++k;
     }

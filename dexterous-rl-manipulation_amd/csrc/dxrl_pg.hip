@@ -1163,10 +1163,8 @@ __device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t nb) {
 // env-major row pitch (floats) of the delta / coefficient rows: the horizon padded to 8 steps,
 // + 4 so the 16 lanes' 16-byte reads start on distinct bank quads (T = 200: pitch 204)
 __host__ __device__ constexpr int64_t gae_pitch(int64_t T) { return (T + 7) / 8 * 8 + 4; }
-// delta + coefficient rows [16][pitch], V_t [T][16], A_t [T8][16] (the padded steps' A land past T)
-__host__ __device__ constexpr int64_t gae_lds_bytes(int64_t T) {
-    return kGlEnvs * (8 * gae_pitch(T) + 4 * T + 4 * ((T + 7) / 8 * 8));
-}
+// delta, coefficient and advantage rows [16][pitch] (env-major), V_t [T][16]
+__host__ __device__ constexpr int64_t gae_lds_bytes(int64_t T) { return kGlEnvs * (12 * gae_pitch(T) + 4 * T); }
 __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict__ rew,
                                                         const uint8_t* __restrict__ done, const float* __restrict__ V,
                                                         int64_t n, int T, float gamma, float lam,
@@ -1177,7 +1175,7 @@ __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict_
     float* Le = gl_lds;                            // [16][P] delta_t (env-major, zero past T)
     float* Ce = Le + kGlEnvs * P;                  // [16][P] c_t
     float* Vs = Ce + kGlEnvs * P;                  // [T][16] V_t (for ret)
-    float* As = Vs + (int64_t)T * kGlEnvs;         // [T8][16] advantages (rows T.. unused)
+    float* Ae = Vs + (int64_t)T * kGlEnvs;         // [16][P] A_t (env-major; the padded steps' A past T)
     __shared__ Moments red[kGlThreads];
     const int tid = threadIdx.x;
     const int64_t grp = DXRL_GAE_XCD ? xcd_contiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
@@ -1232,12 +1230,17 @@ __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict_
             __builtin_amdgcn_sched_barrier(0);  // the loads stay ahead of the chain (the scheduler sank them)
             const float lq[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
             const float cq[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+            float aq[8];
 #pragma unroll
             for (int j = 7; j >= 0; --j) {
-                const float a = lq[j] + cq[j] * next_adv;
-                As[(8 * k + j) * kGlEnvs + e] = a;  // no branch: padded steps land in rows T .. T8 - 1
-                next_adv = a;
+                aq[j] = lq[j] + cq[j] * next_adv;
+                next_adv = aq[j];
             }
+            // the chunk's 8 advantages as two 16-byte stores (8 scalar stores each held the chain
+            // for the store's register read; no branch: padded steps land past T)
+            float4* A4 = reinterpret_cast<float4*>(Ae + e * P + 8 * k);
+            A4[0] = make_float4(aq[0], aq[1], aq[2], aq[3]);
+            A4[1] = make_float4(aq[4], aq[5], aq[6], aq[7]);
             __builtin_amdgcn_sched_barrier(0);
             l0 = nl0;
             l1 = nl1;
@@ -1252,7 +1255,7 @@ __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict_
     for (int64_t q = tid; q < cnt; q += kGlThreads) {
         const int64_t t = q / kGlEnvs, e = q % kGlEnvs;
         if (e0 + e < n) {
-            const float a = As[q];
+            const float a = Ae[e * P + t];
             if (!(DXRL_GAE_DIAG & 4)) {
                 adv[t * n + e0 + e] = a;
                 ret[t * n + e0 + e] = a + Vs[q];

@@ -93,6 +93,11 @@ def parse():
     p.add_argument("--dist", action="store_true",
                    help="create the RCCL process group even at --gpus 1 (before any GPU work) and run the "
                         "multi-rank code path: the trainer's collectives, barrier and max-over-ranks timing")
+    p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                   help="process-group backend: nccl (RCCL over xGMI, one rank per GPU: the driver's scaling "
+                        "runs) or gloo (host-staged exchanges; ranks may share a GPU, rank r on GPU r mod the "
+                        "visible count -- exercises the multi-rank harness on a one-GPU box, not a scaling "
+                        "measurement)")
     a = p.parse_args()
     w = WORKLOADS[a.config]
     a.envs = a.envs or w["envs"]
@@ -107,7 +112,7 @@ def launch_ranks(args) -> int:
     import socket
     import subprocess
     have = torch.cuda.device_count()
-    if have < args.gpus:
+    if have < (1 if args.backend == "gloo" else args.gpus):
         print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {have}", file=sys.stderr)
         return 2
     s = socket.socket()
@@ -123,12 +128,16 @@ def launch_ranks(args) -> int:
 
 def dist_setup(args):
     """One rank per GPU over RCCL (torch.distributed "nccl").  With --dist a world-1 process
-    group is created too, so the collectives run exactly as in a multi-rank job."""
+    group is created too, so the collectives run exactly as in a multi-rank job.  --backend gloo:
+    rank r runs on GPU r mod the visible count (ranks may share one).  Returns (world, rank,
+    device index)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
     if world > 1 or args.dist:
         import socket
         import torch.distributed as dist
@@ -139,7 +148,10 @@ def dist_setup(args):
             os.environ["MASTER_PORT"] = str(s.getsockname()[1])
             s.close()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
+        if args.backend == "gloo":
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -160,7 +172,8 @@ def max_over_ranks(x, world, dev):
     if not _dist_on():
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    gloo = dist.get_backend() == "gloo"  # gloo reduces host tensors
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if gloo else dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -431,6 +444,7 @@ def main():
         cpu = cpu_baseline(args)  # before the GPU is touched (spawned workers)
     world, rank, local = dist_setup(args)
     dev = torch.device("cuda", local if world > 1 else 0)
+    backend = args.backend if world > 1 or args.dist else None
     total_steps = args.envs * world * args.horizon * args.steps
     extra = {}
     if args.learner == "pg":
@@ -447,8 +461,9 @@ def main():
                     f"{args.horizon} env steps x {args.envs} envs + critic fwd + GAE + adv-norm + PPO-clip / value "
                     f"heads + backward + Adam ({upd})")
         dtype = "bf16 MFMA (f32 acc) + f32/f64 env"
-        par = (f"dp{world} (env shards; RCCL all-gather of the f64 advantage moments, all-reduce of the f32 "
-               f"grads)" if world > 1 or args.dist else "dp1")
+        coll = "RCCL" if backend == "nccl" else "gloo (host-staged)"
+        par = (f"dp{world} (env shards; {coll} all-gather of the f64 advantage moments, all-reduce of the f32 "
+               f"grads)" if backend else "dp1")
         extra = {"phases_ms": phases, "mfma": mfma, "train_stats": stats}
     else:
         wall, kernel_ms = rollout_bench(args, world, rank, dev)
@@ -467,7 +482,10 @@ def main():
         "config": {"workload": workload, "learner": args.learner, "envs_per_gpu": args.envs,
                    "global_envs": args.envs * world, "horizon": args.horizon, "parallelism": par,
                    "world_size": world,
-                   "backend": "nccl (RCCL over xGMI)" if world > 1 or args.dist else None,
+                   "backend": {"nccl": "nccl (RCCL over xGMI)", "gloo": "gloo (harness check, ranks may share a GPU)",
+                               None: None}[backend],
+                   "ranks_per_gpu": (world + torch.cuda.device_count() - 1) // torch.cuda.device_count()
+                   if backend == "gloo" else 1,
                    "overlap_comm": bool(args.overlap), "reserve_cus": args.reserve_cus},
     }
     out.update(extra)

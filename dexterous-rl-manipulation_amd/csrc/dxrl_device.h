@@ -44,13 +44,9 @@ __device__ __forceinline__ double clipd(double x, double lo, double hi) {
 struct u32x4 {
     uint32_t x, y, z, w;
 };
-#ifndef DXRL_PHILOX_ROUNDS
-#define DXRL_PHILOX_ROUNDS 10
-#endif
-template <int kRounds = DXRL_PHILOX_ROUNDS>
 __device__ __forceinline__ u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
+    for (int r = 0; r < 10; ++r) {
         // each 32x32 -> 64-bit product as one v_mad_u64_u32 (both halves), not mul_lo + mul_hi
         const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
         const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
@@ -97,13 +93,6 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& n0, fl
     n1 = r * s;
 }
 
-// Rounds of the fused-noise streams (kStreamDyn, kStreamObs: config C5's robustness noise)
-#ifndef DXRL_NOISE_ROUNDS
-#define DXRL_NOISE_ROUNDS 10
-#endif
-constexpr int kNoiseRounds = DXRL_NOISE_ROUNDS;
-__device__ __forceinline__ u32x4 philox_noise(u32x4 c, uint32_t k0, uint32_t k1) { return philox<kNoiseRounds>(c, k0, k1); }
-
 // Stream ids for the Philox counter's third word.
 constexpr uint32_t kStreamReset = 0x52535400u, kStreamPolicy = 0x504f4c00u, kStreamDyn = 0x44594e00u,
                    kStreamObs = 0x4f425300u;
@@ -112,20 +101,17 @@ constexpr uint32_t kStreamReset = 0x52535400u, kStreamPolicy = 0x504f4c00u, kStr
 // Block `blk` of a noise stream (kStreamDyn / kStreamObs) at counter ctr: four standard normals,
 // normal 4 blk + j in nz[j].  Throughput-mode robustness noise has distributional parity with the
 // reference's default_rng normals only (robustness_tests.py:177-207; the host-tape path replays
-// those exactly), so its generator is the build's to choose (DXRL_NOISE_GEN):
-//   0  Philox4x32-R (R = DXRL_NOISE_ROUNDS) and Box-Muller over 24-bit uniforms of (x, y), (z, w);
-//   1  (default, round 5) Philox2x32-10 (Random123: M = 0xD256D193, Weyl 0x9E3779B9) of the
-//      counter (lo ctr, hi ctr << 8 ^ stream ^ blk) under the key k0 ^ k1 * 0x9E3779B9, and
-//      Box-Muller over the 16-bit halves of each output word ((lo, hi) of word 0, then of word 1):
-//      half the 64-bit products per normal.  Config C5 rollout / C2 rollout 1.15 -> 1.12 (A/B,
-//      profiles/r05/ab_c5_noise_generators.log); Box-Muller on the hardware transcendentals
-//      (box_muller_hw, same definition): 1.12 -> 1.10 (profiles/r05/ab_box_muller.log).
-// oracle/dx_oracle.py device_normals_f64 restates both.
-#ifndef DXRL_NOISE_GEN
-#define DXRL_NOISE_GEN 1
-#endif
-constexpr int kNoiseGen = DXRL_NOISE_GEN;
-__device__ __forceinline__ void philox2x32_10(uint32_t& c0, uint32_t& c1, uint32_t k) {
+// those exactly), so its generator is the build's own (round 6):
+//   Philox2x32-10 (Random123: M = 0xD256D193, Weyl 0x9E3779B9) of the counter
+//   (lo ctr, hi ctr << 8 ^ stream ^ blk) under the key k0 ^ k1 * 0x9E3779B9 -> words (w0, w1), and
+//   s = the generator's first word after round 5 of the 10; pair 0 = Box-Muller of w0, pair 1 of
+//   w1: the angle is the word's high 16 bits, the radius uniform the 24-bit integer
+//   (word & 0xFFFF) << 8 | byte of s (byte 0 for w0, byte 1 for w1).
+// The 24-bit radius uniform keeps the normal tail to |z| <= sqrt(-2 ln 2^-24) = 5.77 (round 5 drew
+// it from 16 bits: |z| <= 4.71, a tail quantised to a few radius values above 3.5 sigma).  s costs
+// no product: it is a state the ten rounds pass through anyway, five rounds of mixing from the
+// counter and five from the output words.  oracle/dx_oracle.py device_normals_f64 restates it.
+__device__ __forceinline__ void philox2x32_10(uint32_t& c0, uint32_t& c1, uint32_t k, uint32_t& mid) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         const uint64_t p = (uint64_t)0xD256D193u * c0;  // one v_mad_u64_u32
@@ -133,26 +119,22 @@ __device__ __forceinline__ void philox2x32_10(uint32_t& c0, uint32_t& c1, uint32
         c0 = hi ^ k ^ c1;
         c1 = lo;
         k += 0x9E3779B9u;
+        if (r == 4) mid = c0;
     }
 }
-__device__ __forceinline__ void box_muller16(uint32_t w, float& n0, float& n1) {
-    // u2 = (hi + 1) 2^-16 as 1 + (hi + 1) 2^-16 revolutions (one period on): the bits of hi
-    // placed in the mantissa of 1.0 and 2^-16 added, both exact
+// One Box-Muller pair: angle = the high 16 bits of w, u2 = (hi + 1) 2^-16 as 1 + (hi + 1) 2^-16
+// revolutions (one period on: the bits of hi placed in the mantissa of 1.0 and 2^-16 added, both
+// exact); radius uniform (v24 + 1) 2^-24, v24 = (w & 0xFFFF) << 8 | e (e: one byte of s)
+__device__ __forceinline__ void box_muller24(uint32_t w, uint32_t e, float& n0, float& n1) {
     const float rev = __uint_as_float(0x3F800000u | ((w >> 16) << 7)) + (1.0f / 65536.0f);
-    box_muller_hw<16>(w & 0xFFFFu, rev, n0, n1);
+    box_muller_hw<24>(((w & 0xFFFFu) << 8) | (e & 0xFFu), rev, n0, n1);
 }
 __device__ __forceinline__ void noise_normals4(uint64_t ctr, uint32_t stream, uint32_t blk, uint32_t k0, uint32_t k1,
                                                float nz[4]) {
-    if constexpr (kNoiseGen == 1) {
-        uint32_t c0 = (uint32_t)ctr, c1 = ((uint32_t)(ctr >> 32) << 8) ^ stream ^ blk;
-        philox2x32_10(c0, c1, k0 ^ (k1 * 0x9E3779B9u));
-        box_muller16(c0, nz[0], nz[1]);
-        box_muller16(c1, nz[2], nz[3]);
-    } else {
-        const u32x4 r = philox_noise(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), stream, blk}, k0, k1);
-        box_muller(r.x, r.y, nz[0], nz[1]);
-        box_muller(r.z, r.w, nz[2], nz[3]);
-    }
+    uint32_t c0 = (uint32_t)ctr, c1 = ((uint32_t)(ctr >> 32) << 8) ^ stream ^ blk, s = 0;
+    philox2x32_10(c0, c1, k0 ^ (k1 * 0x9E3779B9u), s);
+    box_muller24(c0, s, nz[0], nz[1]);
+    box_muller24(c1, s >> 8, nz[2], nz[3]);
 }
 
 __device__ __forceinline__ void env_key(uint64_t seed, int64_t gid, uint32_t& k0, uint32_t& k1) {

@@ -78,11 +78,13 @@ __global__ __launch_bounds__(kBlock) void k_reset(EnvSoA s, const uint8_t* __res
 // ME:184-252 fused with the reward plugin.  Block = 256 envs; actions and
 // observations move HBM<->LDS as contiguous float4 streams.
 // Cache policy of the streamed accesses: bit0 = non-temporal stores, bit1 = non-temporal loads.
-// A step whose traffic exceeds the 256 MB Infinity Cache (N >= kNtMinEnvs) streams with both
-// (measured at 2^22 envs: 5.65 TB/s vs 5.26 TB/s plain, interleaved medians of 7); smaller
-// batches keep the default policy so the state stays cache-resident between steps.
+// By batch size (interleaved medians of 7 per N on one box, tools/step_policy_ab.sh,
+// profiles/r06/step_policy_ab*.log): up to 2^19 envs (311 MB of traffic) the default policy
+// (2^19: 0.0525 ms plain vs 0.0615 ms with both non-temporal -- round 5's threshold sat here);
+// from 2^20 non-temporal stores only (0.114 vs 0.119 plain, 0.122 both); from 2^21 both
+// (0.223 vs 0.231 stores only, 0.242 plain; 2^22: 0.444 vs 0.461 / 0.478).
 // DXRL_STEP_VARIANT=0..3 overrides the choice (measurement).
-constexpr int64_t kNtMinEnvs = 1 << 19;
+constexpr int64_t kNtStoreMinEnvs = 1 << 20, kNtLoadMinEnvs = 1 << 21;
 template <int kNt, typename T>
 __device__ __forceinline__ T ld(const T* p) {
     if constexpr ((kNt & 2) != 0) return __builtin_nontemporal_load(p);
@@ -419,7 +421,7 @@ int dxrl_env_step(dxrl_env* env, const float* actions, float* obs, double* rewar
     hipStream_t st = as_stream(stream);
     const int mes = env->cfg.max_episode_steps;
     const char* vs = getenv("DXRL_STEP_VARIANT");
-    const int variant = vs ? atoi(vs) & 3 : (n >= kNtMinEnvs ? 3 : 0);
+    const int variant = vs ? atoi(vs) & 3 : (n >= kNtLoadMinEnvs ? 3 : (n >= kNtStoreMinEnvs ? 1 : 0));
 #define DXRL_STEP_LAUNCH(D, V)                                                                                  \
     hipLaunchKernelGGL((k_step<D, V>), grid, dim3(kBlock), 0, st, env->soa, actions, obs, reward, terminated, \
                        truncated, components, w, mes)

@@ -590,26 +590,17 @@ constexpr int kLYB = kLK * 512, kLXB = kLK * 128, kLSlot = kLYB + kLXB;
 constexpr int kLH1 = kLNB * kLSlot;          // two recomputed H1 chunks [32][256] (h1_swz rows)
 constexpr int kLLds = kLH1 + 2 * kLK * 512;  // 112 KiB at 4 slots
 
-// kNt: non-temporal (the dH2 stream of k_wgrad_l1 is read once: DXRL_WL1_NT)
-template <bool kNt = false>
+// one 16-byte-per-lane LDS-DMA piece (non-temporal loads of the read-once dH2 stream measured
+// within noise, profiles/r05/ab_dh2_nt.log: removed in round 6)
 __device__ __forceinline__ void glds_x4(const void* src, const void* lds_dst) {
     const uint32_t lds_addr =
         __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds_dst);
     uint32_t keep;
-    if (kNt)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(src), "s"(lds_addr)
-                     : "memory");
-    else
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(src), "s"(lds_addr)
-                     : "memory");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_addr)
+                 : "memory");
 }
-#ifndef DXRL_WL1_NT
-#define DXRL_WL1_NT 0
-#endif
 
 // H1 chunk layout: 512-B rows, 16-byte chunk c of row r at c ^ (4 (r & 3) ^ ((r >> 2) & 3)).  The
 // 4 (r & 3) term keeps the transposed reads conflict-free (as tr_frag_swz); the (r >> 2) & 3 term
@@ -705,7 +696,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradPair pr) {
         for (int i = 0; i < 4; ++i) {  // dH2 rows 8 q + 2 i, + 1
             const int prow = 8 * q + 2 * i;
             const int rr = prow + (lane >> 5), gchunk = (lane & 31) ^ (4 * (rr & 3));
-            glds_x4<DXRL_WL1_NT != 0>(Y + (m0 + rr) * ldy + 8 * gchunk, slot + prow * 512);
+            glds_x4(Y + (m0 + rr) * ldy + 8 * gchunk, slot + prow * 512);
         }
         {  // observation rows 8 q .. + 7
             const int row = 8 * q + (lane >> 3), pc = (lane & 7) ^ ((row >> 1) & 7);
@@ -721,7 +712,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_l1(WgradPair pr) {
         for (int i = 0; i < 2; ++i) {  // dH2 rows 4 wave + 2 i, + 1
             const int prow = 4 * wave + 2 * i;
             const int rr = prow + (lane >> 5), gchunk = (lane & 31) ^ (4 * (rr & 3));
-            glds_x4<DXRL_WL1_NT != 0>(Y + (m0 + rr) * ldy + 8 * gchunk, slot + prow * 512);
+            glds_x4(Y + (m0 + rr) * ldy + 8 * gchunk, slot + prow * 512);
         }
         if (lane < 32) {  // observation rows 4 wave .. + 3
             const int row = 4 * wave + (lane >> 3), pc = (lane & 7) ^ ((row >> 1) & 7);

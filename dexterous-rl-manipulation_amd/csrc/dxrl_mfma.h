@@ -90,6 +90,31 @@ __device__ __forceinline__ bf16x8 tr_frag16(const bf16* tile, int col0, int kk, 
     return v;
 }
 
+// tr_frag16 with the k slots of each 8-sample group in even / odd order: lane l gets
+// T[kk + 8 (l >> 4) + e(j)][col0 + (l & 15)], e = (0, 2, 4, 6, 1, 3, 5, 7) -- the first
+// ds_read_b64_tr_b16 reads rows kk + 8 g + 2 q, the second rows kk + 8 g + 2 q + 1.  A weight
+// gradient sums over the samples, so any permutation of the k slots shared by both operands gives
+// the same sum (its f32 order inside the MFMA aside).  Why: a 32-lane bank group of the first read
+// touches rows {0, 2, 4, 6, 8, 10, 12, 14} (+ kk) instead of {0, 1, 2, 3, 8, 9, 10, 11}; at a row
+// pitch of 4 (mod 64) dwords (H1 / H2: 132, X: 36, dout: 20 -> 8 r (mod 64) for the even rows)
+// their 8-dword pieces fill the 64 banks once, where the consecutive rows overlapped 2-way.
+template <int kPitch>
+__device__ __forceinline__ bf16x8 tr_frag16_eo(const bf16* tile, int col0, int kk, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int row = kk + 8 * g + 2 * q;
+    const int col = col0 + 4 * p;
+    lds_bf16* base = (lds_bf16*)(tile);
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + row * kPitch + col));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + (row + 1) * kPitch + col));
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = lo[j];
+        v[4 + j] = hi[j];
+    }
+    return v;
+}
+
 constexpr float k2Log2e = 2.8853900817779268f;  // 2 / ln 2
 
 // Network tanh of the pre-activation acc + b:  1 - 2 / (2^((acc + b) * 2 log2 e) + 1), with the

@@ -504,14 +504,12 @@ struct WsReward {      // an env's dense-reward inputs and episode end of one st
 #ifndef DXRL_WS_OBS_IN_P4
 #define DXRL_WS_OBS_IN_P4 1
 #endif
-// the env wave running the mu head (A/B: its SIMD partner, aux wave kHeadWave + 4, draws beside it)
-#ifndef DXRL_WS_HEAD_WAVE
-#define DXRL_WS_HEAD_WAVE 3
-#endif
 template <bool kNoise, bool kDiag>
 __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p) {
     constexpr int kRows = 32;
-    constexpr int kHeadWave = DXRL_WS_HEAD_WAVE;  // an env wave: the env lanes idle while the head runs
+    // the env wave running the mu head: the env lanes idle while it runs (wave 0 instead, beside
+    // the action-noise wave rather than a reset-draw wave: +-0.5 %, profiles/r05/ab_ws_head_wave_rejected.log)
+    constexpr int kHeadWave = 3;
     // LDS images laid out for conflict-free 16-byte fragment reads (16-lane groups, 64 banks):
     // the read-only W1 / W3 and the observation rows padded to a 40 / 136-dword pitch, the hidden
     // rows unpadded with XOR-swizzled chunks (swz16; the padded 36 / 132-dword pitches of the

@@ -180,9 +180,9 @@ __device__ __forceinline__ void fwd_tiles(const bf16* __restrict__ W, int kst, i
 // instead of MT.  Per output the k order -- and so every bit -- is the same as fwd_run's.
 // (fwd_pipe_w: the same with all KS weight fragments already in registers -- the forward-only
 // pass keeps them resident for the launch)
-template <int KS, int kLda, int MT, typename Epi, typename KHook = NoKHook>
+template <int KS, int kLda, int MT, typename Epi, typename KHook = NoKHook, typename THook = NoKHook>
 __device__ __forceinline__ void fwd_pipe_w(const bf16x8 (&wf)[KS], const bf16* A, int lane, Epi& epi,
-                                           bool no_mfma = false, KHook khook = KHook{}) {
+                                           bool no_mfma = false, KHook khook = KHook{}, THook thook = THook{}) {
     static_assert(KS >= 4 && KS % 4 == 0, "pair schedule assumes KS in {4, 8, 16, ...}");
     const int r = lane & 31, h = lane >> 5;
     constexpr int kPairsPerK = KS >= 8 ? 1 : 8 / KS;  // epilogue pairs issued per k-step
@@ -219,7 +219,10 @@ __device__ __forceinline__ void fwd_pipe_w(const bf16x8 (&wf)[KS], const bf16* A
     }
     epi.prime(MT - 1);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) epi(prev, MT - 1, q);
+    for (int q = 0; q < 8; ++q) {
+        epi(prev, MT - 1, q);
+        thook(q);  // caller work beside the last tile's epilogue (which has no MFMAs of its own)
+    }
 }
 template <int KS, int kLda, int MT, typename Epi, typename Hook = NoHook, typename KHook = NoKHook>
 __device__ __forceinline__ void fwd_pipe(WPre<KS>& w, const bf16* A, int lane, Epi& epi, Hook hook = Hook{},
@@ -287,61 +290,6 @@ struct EpiGate {
         }
     }
 };
-
-// Forward-only pass, both layers software-pipelined across sample tiles (resident W1 / W2, one
-// 32-feature tile per wave).  Stage s = 0 .. MT: L1's chain for sample tile s, then L2's chain for
-// tile s - 1 with, in its MFMA gaps, the tanh epilogues of L2(s - 2) (k-steps 0..7) and of L1(s)
-// (k-steps 8..15); a barrier closes each stage (H1 rows of tile s complete before any wave's
-// L2(s) reads them).  Two waves of a SIMD then never sit in an MFMA-only or VALU-only phase except
-// at the two ends, where the lockstep layer-by-layer form had one of each per layer.  Every output
-// is the same MFMA chain in the same k order and the same epilogue as fwd_pipe_w's, so H1 / H2
-// (and V) are bit for bit the layer-by-layer pass's.
-template <int KS1, int KS2, int MT>
-__device__ __forceinline__ void fwd_xlayer(const bf16x8 (&w1)[KS1], const bf16x8 (&w2)[KS2], const bf16* X, bf16* H1,
-                                           bf16* H2, int lane, int f0, const float* bk2) {
-    static_assert(KS2 == 16, "8 + 8 epilogue pairs over L2's 16 k-steps");
-    const int r = lane & 31, h = lane >> 5;
-    EpiTanh e1{H1, f0, r, nullptr};
-    EpiTanh e2{H2, f0, r, bk2};
-    const bf16* xp = X + r * kXp + 8 * h;
-    const bf16* hp = H1 + r * kHp + 8 * h;
-    f32x16 a1, a2, p2;  // L1(s), L2(s - 1), L2(s - 2)
-    constexpr int kBD = 3;
-#pragma unroll
-    for (int s = 0; s <= MT; ++s) {
-        if (s < MT) {
-            bf16x8 b[KS1];
-#pragma unroll
-            for (int k = 0; k < KS1; ++k) b[k] = *reinterpret_cast<const bf16x8*>(xp + 32 * s * kXp + 16 * k);
-            zero_acc(a1);
-#pragma unroll
-            for (int k = 0; k < KS1; ++k) a1 = mfma32(w1[k], b[k], a1);
-        }
-        if (s == 0) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) e1(a1, 0, q);
-        } else {
-            const bf16* ap = hp + 32 * (s - 1) * kHp;
-            bf16x8 bq[kBD + 1];
-#pragma unroll
-            for (int i = 0; i < kBD; ++i) bq[i] = *reinterpret_cast<const bf16x8*>(ap + 16 * i);
-            zero_acc(a2);
-#pragma unroll
-            for (int k = 0; k < KS2; ++k) {
-                if (k + kBD < KS2) bq[(k + kBD) % (kBD + 1)] = *reinterpret_cast<const bf16x8*>(ap + 16 * (k + kBD));
-                __builtin_amdgcn_sched_barrier(0);
-                a2 = mfma32(w2[k], bq[k % (kBD + 1)], a2);
-                if (k < 8 && s >= 2) e2(p2, s - 2, k);
-                if (k >= 8 && s < MT) e1(a1, s, k - 8);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            p2 = a2;
-        }
-        if (s < MT) __syncthreads();  // (after the last stage the head's barrier follows the tail)
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) e2(p2, MT - 1, q);
-}
 
 // tanh(acc + bias) -> bf16 row-major activation tile (4 consecutive features per 8-byte store)
 // (bk: the lane's 16 pre-scaled biases tanh_bias(b[32 ft + 8 g + 4 h + u]) at [4 g + u], or null)
@@ -413,24 +361,9 @@ __device__ __forceinline__ void copy_tile_out_n(const bf16* T, bf16* out, int64_
     }
 }
 
-// One 16-byte chunk of the dH2 tile to HBM, a plain store.  DXRL_DH2_NT=1 stores it non-temporal
-// (written through instead of left dirty in the caches, so k_wgrad_l1's read-back does not also
-// pay for the write-back of the lines it evicts: a 524 MB LDS-DMA stream runs at 6.1 TB/s after
-// nt stores and at 4.0 TB/s after plain ones, tools/stream_mb.hip).  Not the default: +1-1.7 % on
-// most boxes, -10 % on others, all kernels of the iteration slower there
-// (profiles/r05/ab_dh2_nt.log).
-#ifndef DXRL_DH2_NT
-#define DXRL_DH2_NT 0
-#endif
-__device__ __forceinline__ void store_dh2(bf16* dst, const bf16x8& v) {
-    if (DXRL_DH2_NT) {
-        typedef unsigned int u32v4 __attribute__((ext_vector_type(4)));
-        __builtin_nontemporal_store(__builtin_bit_cast(u32v4, v),
-                                    (__attribute__((address_space(1))) u32v4*)dst);
-    } else {
-        *(__attribute__((address_space(1))) bf16x8*)dst = v;
-    }
-}
+// One 16-byte chunk of the dH2 tile to HBM, a plain store (non-temporal stores were measured +1-1.7 %
+// on most boxes and -10 % on others, profiles/r05/ab_dh2_nt.log: removed in round 6)
+__device__ __forceinline__ void store_dh2(bf16* dst, const bf16x8& v) { *(__attribute__((address_space(1))) bf16x8*)dst = v; }
 
 // Hide a pointer's provenance from the optimiser so loads through it are not hoisted
 // out of the tile loop (loop-invariant weight / bias loads would otherwise pin registers
@@ -484,12 +417,31 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #ifndef DXRL_FWD_EARLY_X
 #define DXRL_FWD_EARLY_X 1
 #endif
-// forward-only pass with resident weights: L1 / L2 pipelined across sample tiles (fwd_xlayer);
-// measured 3 % slower than layer by layer (158.5 vs 154 us, bit-identical: four more barriers
-// per tile cost more than the overlap wins; profiles/r05/ab_fwd_xlayer_rejected.log) -- off
-#ifndef DXRL_FWD_XLAYER
-#define DXRL_FWD_XLAYER 0
+// train passes: all 16 W2 fragments of the wave's feature tile issued at the start of L1 and all 16
+// W2T fragments at the start of the dW3 / dH2 phase (a phase ahead of their layer, held in
+// registers: L2 and dH1 then open with their whole weight slice on chip instead of streaming
+// half of it from L2 behind their first MFMAs)
+#ifndef DXRL_EARLY_W
+#define DXRL_EARLY_W 3  // bit 0: W2 under L1, bit 1: W2T under dW3 / dH2
 #endif
+
+// dW1 without the barrier after dH1: a wave's dW1 reads only its own dH1 columns (and X), so the
+// MFMAs of the first three 32-sample blocks issue beside dH1's last epilogue (VALU only) and the
+// db2 column sums' second stage moves behind the end-of-tile barrier
+#ifndef DXRL_DW1_TAIL
+#define DXRL_DW1_TAIL 1
+#endif
+
+// dW3 / dW1 operands through tr_frag16_eo (even / odd sample order inside each 8-sample group:
+// the transposed reads conflict-free) instead of tr_frag16 (2-way)
+#ifndef DXRL_TR_EO
+#define DXRL_TR_EO 1
+#endif
+template <int kPitch>
+__device__ __forceinline__ bf16x8 wg_frag(const bf16* tile, int col0, int kk, int lane) {
+    if constexpr (DXRL_TR_EO) return tr_frag16_eo<kPitch>(tile, col0, kk, lane);
+    else return tr_frag16<kPitch>(tile, col0, kk, lane);
+}
 
 // kFW waves per workgroup: 4 (one per SIMD, 512 registers each) or 8 (two per SIMD)
 // kTrain: forward + heads + backward; otherwise the forward-only critic-value pass, which keeps
@@ -589,7 +541,9 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     // 160 KB of weight fragments from L2 per tile and workgroup
     constexpr bool kResW = !kTrain && kNT == 1 && DXRL_FWD_RESIDENT_W && DXRL_L2_PIPE;
     constexpr bool kEarlyX = kResW && DXRL_FWD_EARLY_X;
-    constexpr bool kXL = kResW && DXRL_FWD_XLAYER;  // both layers pipelined across sample tiles
+    constexpr bool kDw1Tail = kTrain && kNT == 1 && kMT == 4 && DXRL_EARLY_W >= 2 && DXRL_DW1_TAIL && DXRL_DH2_IN_DH1;
+    constexpr bool kEarlyW = kTrain && kNT == 1 && (DXRL_EARLY_W & 1);
+    constexpr bool kEarlyWT = kTrain && kNT == 1 && (DXRL_EARLY_W & 2);
     bf16x8 w1res[kResW ? kIn / 16 : 1], w2res[kResW ? kH / 16 : 1];
     if constexpr (kResW) {
         const gbf16x8* p1 = (const gbf16x8*)p.W1 + (int64_t)ft0 * (kIn / 16) * 64 + lane;
@@ -673,22 +627,25 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // HBM load issued here would make every weight-fragment wait below wait for it too)
 
         // ---- L1, L2 (wave w: hidden features 64w .. 64w + 63, all 128 samples)
-        if constexpr (kXL) {
-            fwd_xlayer<kIn / 16, kH / 16, kMT>(w1res, w2res, X, H1, H2, lane, 32 * ft0 + 4 * h, bkres);
-        } else {
+        bf16x8 w2e[kEarlyW ? kH / 16 : 1];  // kEarlyW: this wave's W2 slice, in flight under L1
+        if constexpr (kEarlyW) {
+            const gbf16x8* wp = (const gbf16x8*)W2 + (int64_t)ft0 * (kH / 16) * 64 + lane;
+#pragma unroll
+            for (int k = 0; k < kH / 16; ++k) w2e[k] = wp[64 * k];
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll 1
-            for (int j = 0; j < kNT; ++j) {
-                // bias = W1 column 45 (X column 45 = 1)
-                if (j > 0) w_prefetch(pw1, W1, kIn / 16, ft0 + j, lane);
-                EpiTanh e1{H1, 32 * (ft0 + j) + 4 * h, r, nullptr};
-                fwd_pipe<kIn / 16, kXp, kMT>(pw1, X, lane, e1);
-            }
+        for (int j = 0; j < kNT; ++j) {
+            // bias = W1 column 45 (X column 45 = 1)
+            if (j > 0) w_prefetch(pw1, W1, kIn / 16, ft0 + j, lane);
+            EpiTanh e1{H1, 32 * (ft0 + j) + 4 * h, r, nullptr};
+            fwd_pipe<kIn / 16, kXp, kMT>(pw1, X, lane, e1);
         }
         // the first W2 fragments go out before the barrier (their L2 latency overlaps its wait)
         WPre<kH / 16> pw2;
-        if constexpr (!kResW) w_prefetch(pw2, W2, kH / 16, ft0, lane);
+        if constexpr (!kResW && !kEarlyW) w_prefetch(pw2, W2, kH / 16, ft0, lane);
         STAMP(2);
-        if constexpr (!kXL) __syncthreads();
+        __syncthreads();
         STAMP(3);
         // head inputs (HBM), issued halfway through L2 so their latency hides behind its second half
         const int ml = 32 * wave + r;
@@ -732,7 +689,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             }
         };
 #pragma unroll 1
-        for (int j = 0; j < (kXL ? 0 : kNT); ++j) {
+        for (int j = 0; j < kNT; ++j) {
             bft = ft0 + j;
             const auto l2_hook = [&]() {
                 if (j == kNT - 1) head_inputs();
@@ -749,6 +706,9 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             if constexpr (kResW) {  // biases and head inputs resident: nothing to load
                 EpiTanh e2r{H2, 32 * (ft0 + j) + 4 * h, r, bkres};
                 fwd_pipe_w<kH / 16, kHp, kMT>(w2res, H1, lane, e2r, (diag & 32) != 0);
+            } else if constexpr (kEarlyW) {  // the W2 slice is in registers: the head inputs go out now
+                l2_hook();
+                fwd_pipe_w<kH / 16, kHp, kMT>(w2e, H1, lane, e2, (diag & 32) != 0);
             } else {
                 fwd_pipe<kH / 16, kHp, kMT>(pw2, H1, lane, e2, l2_hook, (diag & 32) != 0);
             }
@@ -1048,27 +1008,47 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         __syncthreads();
         STAMP(8);
 
+        bf16x8 w2te[kEarlyWT ? kH / 16 : 1];  // kEarlyWT: this wave's W2T slice, in flight under dW3 / dH2
+        if constexpr (kEarlyWT) {
+            const gbf16x8* wp = (const gbf16x8*)W2T + (int64_t)ft0 * (kH / 16) * 64 + lane;
+#pragma unroll
+            for (int k = 0; k < kH / 16; ++k) w2te[k] = wp[64 * k];
+            __builtin_amdgcn_sched_barrier(0);
+        }
         // ---- dW3 += dout^T H2 (wave w: H2 columns of its tiles), then dH2 in place of H2
 #pragma unroll
         for (int kk = 0; kk < kTR; kk += 32) {
-            const bf16x8 a = tr_frag16<kDp>(D, 0, kk, lane);
+            const bf16x8 a = wg_frag<kDp>(D, 0, kk, lane);
 #pragma unroll
             for (int j = 0; j < kNT; ++j)
 #pragma unroll
                 for (int ci = 0; ci < 2; ++ci)
                     if (!(diag & 4))
-                        acc3[j][ci] = mfma16(a, tr_frag16<kHp>(H2, 32 * (ft0 + j) + 16 * ci, kk, lane), acc3[j][ci]);
+                        acc3[j][ci] = mfma16(a, wg_frag<kHp>(H2, 32 * (ft0 + j) + 16 * ci, kk, lane), acc3[j][ci]);
         }
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
-            f32x16 acc[kMT];
             // dH2^T = W3^T dout^T over head rows 0..15 (dout rows 16..31 are zero)
-            if (j == 0) fwd_run<1, kDp, kMT>(pw3t, D, acc, lane);
-            else fwd_tiles<1, kDp, kMT>(W3T, kOut / 16, ft0 + j, D, acc, lane);
-            gate_in_place(acc, ft0 + j, H2, lane);
+            if constexpr (kEarlyWT) {
+                // one 32-sample tile at a time (one accumulator live beside the W2T slice in flight;
+                // the same single MFMA per tile as fwd_run<1>, so the same bits)
+                const bf16* ap = D + r * kDp + 8 * h;
+#pragma unroll
+                for (int mt = 0; mt < kMT; ++mt) {
+                    f32x16 acc1[1];
+                    zero_acc(acc1[0]);
+                    acc1[0] = mfma32(pw3t.wf[0], *reinterpret_cast<const bf16x8*>(ap + 32 * mt * kDp), acc1[0]);
+                    gate_in_place(acc1, ft0 + j, H2 + 32 * mt * kHp, lane);
+                }
+            } else {
+                f32x16 acc[kMT];
+                if (j == 0) fwd_run<1, kDp, kMT>(pw3t, D, acc, lane);
+                else fwd_tiles<1, kDp, kMT>(W3T, kOut / 16, ft0 + j, D, acc, lane);
+                gate_in_place(acc, ft0 + j, H2, lane);
+            }
         }
         WPre<kH / 16> pw2t;  // dH1's first W2T fragments, ahead of the barrier
-        w_prefetch(pw2t, W2T, kH / 16, ft0, lane);
+        if constexpr (!kEarlyWT) w_prefetch(pw2t, W2T, kH / 16, ft0, lane);
         STAMP(9);
         __syncthreads();
         STAMP(10);
@@ -1106,37 +1086,64 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 const bf16x8 v = *reinterpret_cast<const bf16x8*>(H2 + row * kHp + col);
                 if (m0 + row < p.rows) store_dh2(p.dh2_out + (m0 + row) * kH + col, v);
             };
-            fwd_pipe<kH / 16, kHp, kMT>(pw2t, H2, lane, eg, NoHook{}, false, copy_k);
+            if constexpr (kDw1Tail) {
+                // dW1 of sample blocks 0..2 (gated during the tile loop) beside the tail epilogue
+                // of block 3; block 3's dW1 follows it (same MFMAs, same kk order as below)
+                const auto dw1_tail = [&](int q) {
+                    if (q != 1 && q != 3 && q != 5) return;
+                    const int kk = 32 * (q >> 1);
+                    if (kk == 0 && tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
+                    bf16x8 b[3];
+#pragma unroll
+                    for (int ci = 0; ci < 3; ++ci) b[ci] = wg_frag<kXp>(X, 16 * ci, kk, lane);
+#pragma unroll
+                    for (int ri = 0; ri < 2; ++ri) {
+                        const bf16x8 a = wg_frag<kHp>(H1, 32 * ft0 + 16 * ri, kk, lane);
+#pragma unroll
+                        for (int ci = 0; ci < 3; ++ci)
+                            if (!(diag & 4)) acc1[0][ri][ci] = mfma16(a, b[ci], acc1[0][ri][ci]);
+                    }
+                };
+                fwd_pipe_w<kH / 16, kHp, kMT>(w2te, H2, lane, eg, false, copy_k, dw1_tail);
+            } else if constexpr (kEarlyWT) {
+                fwd_pipe_w<kH / 16, kHp, kMT>(w2te, H2, lane, eg, false, copy_k);
+            } else {
+                fwd_pipe<kH / 16, kHp, kMT>(pw2t, H2, lane, eg, NoHook{}, false, copy_k);
+            }
 #else
             fwd_pipe<kH / 16, kHp, kMT>(pw2t, H2, lane, eg);
 #endif
         }
         STAMP(11);
-        __syncthreads();
-        STAMP(12);
-
-        // ---- dW1 += dH1^T X (wave w: hidden rows of its tiles, input columns 0..63); LDS only,
-        //      so the next tile's X loads go out now
-        if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
-#if !DXRL_DH2_IN_DH1
-        // dH2 tile -> HBM (Y of the dW2 GEMM; H2 holds dH2 until the next tile's L2)
-        copy_tile_out_n<kFThreads, kTR>(H2, p.dh2_out, kH, m0, p.rows, tid, diag);
-#endif
-        if (tid < kH) {  // db2 stage 2: the kFW row-group sums of column tid, in row order
-            const float* cs = reinterpret_cast<const float*>(lds + kOffD);
+        const auto db2_stage2 = [&]() {
+            if (tid < kH) {  // db2 stage 2: the kFW row-group sums of column tid, in row order
+                const float* cs = reinterpret_cast<const float*>(lds + kOffD);
 #pragma unroll
-            for (int w = 0; w < kFW; ++w) db2 += cs[w * kH + tid_l];
+                for (int w = 0; w < kFW; ++w) db2 += cs[w * kH + tid_l];
+            }
+        };
+        if constexpr (!kDw1Tail) {
+            __syncthreads();
+            STAMP(12);
+            // ---- dW1 += dH1^T X (wave w: hidden rows of its tiles, input columns 0..63); LDS only,
+            //      so the next tile's X loads go out now
+            if (tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
+#if !DXRL_DH2_IN_DH1
+            // dH2 tile -> HBM (Y of the dW2 GEMM; H2 holds dH2 until the next tile's L2)
+            copy_tile_out_n<kFThreads, kTR>(H2, p.dh2_out, kH, m0, p.rows, tid, diag);
+#endif
+            db2_stage2();
         }
 #pragma unroll
-        for (int kk = 0; kk < kTR; kk += 32) {
+        for (int kk = kDw1Tail ? 96 : 0; kk < kTR; kk += 32) {
             bf16x8 b[3];
 #pragma unroll
-            for (int ci = 0; ci < 3; ++ci) b[ci] = tr_frag16<kXp>(X, 16 * ci, kk, lane);
+            for (int ci = 0; ci < 3; ++ci) b[ci] = wg_frag<kXp>(X, 16 * ci, kk, lane);
 #pragma unroll
             for (int j = 0; j < kNT; ++j)
 #pragma unroll
                 for (int ri = 0; ri < 2; ++ri) {
-                    const bf16x8 a = tr_frag16<kHp>(H1, 32 * (ft0 + j) + 16 * ri, kk, lane);
+                    const bf16x8 a = wg_frag<kHp>(H1, 32 * (ft0 + j) + 16 * ri, kk, lane);
 #pragma unroll
                     for (int ci = 0; ci < 3; ++ci)
                         if (!(diag & 4)) acc1[j][ri][ci] = mfma16(a, b[ci], acc1[j][ri][ci]);
@@ -1145,6 +1152,9 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         STAMP(13);
         __syncthreads();
         STAMP(14);
+        // (kDw1Tail: the dout region holding the row-group sums is not written again before the
+        // next tile's head, two barriers on)
+        if constexpr (kDw1Tail) db2_stage2();
     }
     if ((diag & 8) && lane == 0) {
 #pragma unroll
@@ -1672,8 +1682,12 @@ int dxrl_pg_fused_pair_gnorm(int32_t device, const dxrl_pg_fused_args* c, const 
     DXRL_REQUIRE(c->dh2 && a->dh2 && c->dh2 != a->dh2 && c->partial && a->partial && c->partial != a->partial &&
                      c->wgrad_partial && a->wgrad_partial && c->wgrad_partial != a->wgrad_partial,
                  "fused_pair: each pass needs its own dh2, partial and wgrad_partial buffers");
-    DXRL_REQUIRE(c->wgrad_splits > kReduceGroups && a->wgrad_splits > kReduceGroups,
-                 "fused_pair: wgrad_splits > %d per network", kReduceGroups);
+    // the dW2 launch caps each split count at the 32-row chunk count (launch_wgrad_l1_pair): the
+    // capped counts must still exceed kReduceGroups (checked after the launches, a
+    // small batch overwrote dH2's partial slabs -- or dW2 itself at one split -- before failing)
+    DXRL_REQUIRE(c->wgrad_splits > kReduceGroups && a->wgrad_splits > kReduceGroups &&
+                     c->rows / 32 > kReduceGroups,
+                 "fused_pair: wgrad_splits > %d per network and rows / 32 > %d", kReduceGroups, kReduceGroups);
     DXRL_REQUIRE(c->act == nullptr || (reinterpret_cast<uintptr_t>(c->act) & 15) == 0, "fused_pair: alignment");
     for (const dxrl_pg_fused_args* x : {c, a}) {
         DXRL_REQUIRE(x->packed && x->params && x->obs && x->loss_partial && x->grid >= 1 && x->grid <= 65535,
@@ -1699,7 +1713,7 @@ int dxrl_pg_fused_pair_gnorm(int32_t device, const dxrl_pg_fused_args* c, const 
                                       a->wgrad_partial, G + kOffW2a, kH, static_cast<const bf16*>(a->obs), kIn, a->rows,
                                       kHx, st, &ns_c, &ns_a))
         return rc;
-    DXRL_REQUIRE(ns_c > kReduceGroups && ns_a > kReduceGroups, "fused_pair: too few rows for the splits");
+    // (ns_c, ns_a = min(splits, rows / 32) > kReduceGroups by the checks above)
     if (gnorm_partial) *gnorm_blocks = 2 * (nb1 + nb2);
     GradReduceNet rc_{reinterpret_cast<const float4*>(c->partial), grid_c, G + kOffW1c, G + kOffW3c, nullptr,
                       G + kOffW2c, (float)c->ent_coef, reinterpret_cast<const float4*>(c->wgrad_partial), ns_c,

@@ -96,10 +96,14 @@ class TrainerConfig:
     # both train passes of a step through dxrl_pg_fused_pair: their dW2 contractions in one launch
     # (learner CUs / 2 splits each instead of every CU per network: half the split-K slab traffic)
     # and both reductions in one launch (needs the fused learner with on-chip H1, serialised
-    # exchanges, and > 16 row chunks per split); False: one dxrl_pg_fused call per network
+    # exchanges, and more than 16 splits per network after the cap below); False: one
+    # dxrl_pg_fused call per network.  Memory: the critic's own dH2 ([M][256] bf16, 0.42 GB at
+    # C2's 819,200 samples) and fused-partial slab, and 2 x pair_splits [256][256] f32 dW2 slabs
+    # (64 MB at 128 splits); the per-network path's [splits + 16][256][288] slab is then not
+    # allocated unless a per-network pass runs
     pair_learner: bool = True
-    # dW2 splits per network of the paired step (0: learner CUs / 2, capped by the smallest
-    # minibatch slice's 32-row chunks / 17)
+    # dW2 splits per network of the paired step (0: learner CUs / 2), capped at the smallest
+    # minibatch slice's 32-row chunk count; the paired step needs the capped count > 16
     pair_splits: int = 0
     # one rank, paired step: the pair's reduction also writes the grad-norm partials
     # (dxrl_pg_fused_pair_gnorm) and the optimiser step finishes the norm from them
@@ -240,7 +244,7 @@ class PGTrainer:
         self.splits = max(1, min(cfg.splitk_target_blocks // 3, M // 1024))
         if self.learner_cus < cus:
             self.splits = min(self.splits, self.learner_cus)
-        self.kpartial = z(self.splits + 16, H, HX)  # + two-level reduction scratch
+        self._kpartial = None  # [splits + 16][256][288] f32, allocated on first use (kpartial)
         self.gnorm2 = torch.zeros(1, dtype=torch.float64, device=d)
         tr_, pf_ = C.c_int32(), C.c_int64()
         N.call("dxrl_pg_fused_sizes", C.byref(tr_), C.byref(pf_))
@@ -271,6 +275,19 @@ class PGTrainer:
             N.call("dxrl_pg_gnorm_blocks", C.byref(nbk))
             self.gn_partial = torch.zeros(nbk.value, dtype=torch.float64, device=d)
         self.pack()
+
+    @property
+    def kpartial(self):
+        """Split-K partial slabs of the per-network dW2 paths (+ two-level reduction scratch):
+        allocated on first use, so a paired-step trainer that never runs a per-network pass does
+        not hold them."""
+        if self._kpartial is None:
+            self._kpartial = torch.zeros(self.splits + 16, H, HX, dtype=torch.float32, device=self.dev)
+        return self._kpartial
+
+    @kpartial.setter
+    def kpartial(self, t):
+        self._kpartial = t
 
     # ------------------------------------------------------------------ params
     def _view(self, t, off, rows, cols):

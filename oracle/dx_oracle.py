@@ -445,21 +445,7 @@ def philox_reset_draws(cur: OracleCurriculum, k0: int, k1: int, ctr: int) -> np.
 STREAM_POLICY, STREAM_DYN, STREAM_OBS = 0x504F4C00, 0x44594E00, 0x4F425300  # csrc/dxrl_device.h kStream*
 
 
-def philox4x32_10_np(c0, c1, c2, c3, k0, k1):
-    """Vectorised philox4x32_10 over NumPy arrays (uint64 lanes holding u32 values)."""
-    m = np.uint64(_U32)
-    x, y, z, w = (np.asarray(v, np.uint64) & m for v in (c0, c1, c2, c3))
-    k0 = np.asarray(k0, np.uint64) & m
-    k1 = np.asarray(k1, np.uint64) & m
-    for _ in range(10):
-        p0, p1 = np.uint64(_PH_M0) * x, np.uint64(_PH_M1) * z
-        x, y, z, w = ((p1 >> np.uint64(32)) ^ y ^ k0) & m, p1 & m, ((p0 >> np.uint64(32)) ^ w ^ k1) & m, p0 & m
-        k0, k1 = (k0 + np.uint64(_PH_W0)) & m, (k1 + np.uint64(_PH_W1)) & m
-    return x, y, z, w
-
-
 _P2_M, _P2_W = 0xD256D193, 0x9E3779B9
-NOISE_GEN = 1  # csrc/dxrl_device.h DXRL_NOISE_GEN: the fused-noise generator the build uses
 
 
 def philox2x32_10(ctr, key):
@@ -474,47 +460,44 @@ def philox2x32_10(ctr, key):
     return x, y
 
 
-def philox2x32_10_np(c0, c1, k):
-    """Vectorised philox2x32_10 over NumPy arrays (uint64 lanes holding u32 values)."""
+def philox2x32_10_np(c0, c1, k, mid_round: int = -1):
+    """Vectorised philox2x32_10 over NumPy arrays (uint64 lanes holding u32 values).  With
+    ``mid_round`` r >= 0 also returns the first word after round r + 1 (the device's ``mid``)."""
     m = np.uint64(_U32)
     x, y = (np.asarray(v, np.uint64) & m for v in (c0, c1))
     k = np.asarray(k, np.uint64) & m
-    for _ in range(10):
+    mid = None
+    for r in range(10):
         p = np.uint64(_P2_M) * x
         x, y = ((p >> np.uint64(32)) ^ k ^ y) & m, p & m
         k = (k + np.uint64(_P2_W)) & m
-    return x, y
+        if r == mid_round:
+            mid = x
+    return (x, y) if mid_round < 0 else (x, y, mid)
 
 
-def device_normals_f64(key, ctr, stream: int, blocks: int, gen: int = NOISE_GEN) -> np.ndarray:
+def device_normals_f64(key, ctr, stream: int, blocks: int) -> np.ndarray:
     """The device's fused-noise normals (csrc/dxrl_device.h noise_normals4: block b gives
-    normals 4b .. 4b+3), restated in f64 with libm.  gen 1 (the build's): Philox2x32-10 of
-    (lo ctr, hi ctr << 8 ^ stream ^ b) under k0 ^ k1 * 0x9E3779B9, Box-Muller (r cos, r sin) over
-    the 16-bit halves (lo, hi) of word 0, then of word 1; gen 0: Philox4x32-10 of (lo ctr, hi ctr,
-    stream, b), Box-Muller over the 24-bit uniforms of (x, y), then (z, w).  The device evaluates
-    them with hardware log / sqrt / sin / cos in f32, so the values agree to ~1e-6 relative, not
-    bit for bit: the tests use this to pin WHICH draws (key, counter, stream, block) a kernel
-    consumed.  ``ctr``: uint64 array; ``key``: (k0, k1) arrays broadcastable to it.  Returns f64
-    [..., 4 * blocks]."""
+    normals 4b .. 4b+3), restated in f64 with libm: Philox2x32-10 of (lo ctr, hi ctr << 8 ^
+    stream ^ b) under k0 ^ k1 * 0x9E3779B9 -> (w0, w1), s = the first word after round 5;
+    Box-Muller (r cos, r sin) of w0, then of w1, each with the angle u2 = (high 16 bits + 1) 2^-16
+    and the radius uniform u1 = (v24 + 1) 2^-24, v24 = (word & 0xFFFF) << 8 | byte j of s (j = 0
+    for w0, 1 for w1).  The device evaluates them with hardware log / sqrt / sin / cos in f32, so
+    the values agree to ~1e-6 relative, not bit for bit: the tests use this to pin WHICH draws
+    (key, counter, stream, block) a kernel consumed.  ``ctr``: uint64 array; ``key``: (k0, k1)
+    arrays broadcastable to it.  Returns f64 [..., 4 * blocks]."""
     ctr = np.asarray(ctr, np.uint64)
     m = np.uint64(_U32)
     out = []
     for b in range(blocks):
-        if gen == 1:
-            k = (np.asarray(key[0], np.uint64) ^ ((np.asarray(key[1], np.uint64) * np.uint64(_P2_W)) & m)) & m
-            c1 = (((ctr >> np.uint64(32)) << np.uint64(8)) ^ np.uint64(stream) ^ np.uint64(b)) & m
-            w0, w1 = philox2x32_10_np(ctr & m, c1, np.broadcast_to(k, ctr.shape))
-            pairs = [((w & np.uint64(0xFFFF)), (w >> np.uint64(16))) for w in (w0, w1)]
-            scale = 1.0 / 65536.0
-            pairs = [(((lo.astype(np.float64) + 1.0) * scale), ((hi.astype(np.float64) + 1.0) * scale))
-                     for lo, hi in pairs]
-        else:
-            x, y, z, w = philox4x32_10_np(ctr & m, ctr >> np.uint64(32), np.full(ctr.shape, stream),
-                                          np.full(ctr.shape, b), key[0], key[1])
-            scale = 1.0 / 16777216.0
-            pairs = [(((a_ >> np.uint64(8)).astype(np.float64) + 1.0) * scale,
-                      ((b_ >> np.uint64(8)).astype(np.float64) + 1.0) * scale) for a_, b_ in ((x, y), (z, w))]
-        for ua, ub in pairs:
+        k = (np.asarray(key[0], np.uint64) ^ ((np.asarray(key[1], np.uint64) * np.uint64(_P2_W)) & m)) & m
+        c1 = (((ctr >> np.uint64(32)) << np.uint64(8)) ^ np.uint64(stream) ^ np.uint64(b)) & m
+        w0, w1, s = philox2x32_10_np(ctr & m, c1, np.broadcast_to(k, ctr.shape), mid_round=4)
+        for j, w in enumerate((w0, w1)):
+            e = (s >> np.uint64(8 * j)) & np.uint64(0xFF)
+            v24 = ((w & np.uint64(0xFFFF)) << np.uint64(8)) | e
+            ua = (v24.astype(np.float64) + 1.0) / 16777216.0
+            ub = ((w >> np.uint64(16)).astype(np.float64) + 1.0) / 65536.0
             r = np.sqrt(-2.0 * np.log(ua))
             ang = 6.283185307179586 * ub
             out += [r * np.cos(ang), r * np.sin(ang)]

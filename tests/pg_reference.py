@@ -148,3 +148,24 @@ def autograd_loss(params, obs_rm, act, logp_old, rew, done, n, T, cfg):
         ls.sum() + 0.5 * ACT * (1 + LOG2PI))
     loss.backward()
     return params.grad.detach()
+
+
+def fp64_pin(got_grads, got_V, got_adv, params, obs_rm, act, logp_old, rew, done, n, T, cfg, g_bf16, info_bf16,
+             factor=1.5, blocks=("W1a", "W2a", "W3a", "W1c", "W2c", "W3c")):
+    """Pin the HIP learner to fp64 truth, not just to the bf16 restatement:
+    the same objective on the same tapes in float64 with no bf16 rounding anywhere is the truth;
+    for every gradient block and for V / adv the HIP result's distance to it must be at most
+    `factor` x the bf16-emulating torch reference's distance (both carry the same bf16 storage
+    points, so a kernel regression that adds error shows as a ratio above 1).  Returns the
+    ratios {name: |hip - truth| / |bf16 ref - truth|}."""
+    g64, info64 = loss_and_grads(params.double(), obs_rm, act, logp_old, rew, done, n, T, cfg, bf16=False)
+    got_b, ref_b, tru_b = unpack(got_grads), unpack(g_bf16), unpack(g64)
+    ratios = {}
+    pairs = [(b, got_b[b].double(), ref_b[b].double(), tru_b[b]) for b in blocks]
+    pairs += [("V", got_V.double(), info_bf16["V"].double(), info64["V"]),
+              ("adv", got_adv.double(), info_bf16["adv"].double(), info64["adv"])]
+    for name, got, ref, tru in pairs:
+        e_hip, e_ref = (got - tru).norm().item(), (ref - tru).norm().item()
+        ratios[name] = e_hip / max(e_ref, 1e-300)
+        assert e_hip <= factor * e_ref, (name, e_hip, e_ref)
+    return ratios

@@ -189,12 +189,14 @@ def test_large_batch_vs_oracle(pkg):
 
 
 def test_streaming_step_policy_is_bit_identical(pkg, monkeypatch):
-    """N >= 2^19 steps stream with non-temporal loads/stores (dxrl_env.hip kNtMinEnvs); the
-    results are the default-policy kernel's bit for bit, and sampled lanes match the oracle."""
-    n, T = (1 << 19) + 37, 4
+    """Large batches stream with non-temporal stores (N >= 2^20) and loads (N >= 2^21;
+    dxrl_env.hip kNtStoreMinEnvs / kNtLoadMinEnvs); every policy variant (0 plain, 1 nt stores,
+    2 nt loads, 3 both) gives the default-policy kernel's results bit for bit, and sampled lanes
+    match the oracle."""
+    n, T = (1 << 21) + 37, 4
     dev = torch.device("cuda:0")
     envs = []
-    for v in ("0", "3"):
+    for v in ("0", "1", "2", "3"):
         e = pkg.envs.VecEnv(n, curriculum_config=pkg.experiments.CurriculumConfig.variable(), reward_type="dense",
                             seed=77, device=dev)
         e.reset(write_obs=False)
@@ -207,16 +209,17 @@ def test_streaming_step_policy_is_bit_identical(pkg, monkeypatch):
         for v, e in envs:
             monkeypatch.setenv("DXRL_STEP_VARIANT", v)
             outs[v] = [x.clone() for x in e.step(a)]
-        for x, y in zip(outs["0"], outs["3"]):
-            assert torch.equal(x, y)
+        for v in ("1", "2", "3"):
+            for x, y in zip(outs["0"], outs[v]):
+                assert torch.equal(x, y), v
     monkeypatch.delenv("DXRL_STEP_VARIANT")
-    e = envs[1][1]
+    e = envs[3][1]
     a = (torch.rand(n, 15, generator=g, device=dev) * 2.6 - 1.3).contiguous()
     jp, jv = e.joint_positions.cpu().numpy(), e.joint_velocities.cpu().numpy()
     op, ov = e.object_position.cpu().numpy(), e.object_velocity.cpu().numpy()
     size, fric, mass = (x.cpu().numpy() for x in (e.object_size, e.friction_coefficient, e.object_mass))
     flags, tcount = e.flags.cpu().numpy(), e.step_count.cpu().numpy()
-    ob, rw, te, tr = (x.cpu().numpy() for x in e.step(a))  # default policy at this N: streaming
+    ob, rw, te, tr = (x.cpu().numpy() for x in e.step(a))  # default policy at this N: both non-temporal
     an = a.cpu().numpy()
     for i in [0, 1, 255, 256, 4097, n // 2, n - 1]:
         o = OracleEnv(cur=OracleCurriculum(object_size=size[i], friction_coefficient=fric[i], object_mass=mass[i]))

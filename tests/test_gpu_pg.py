@@ -131,6 +131,9 @@ def test_iteration_matches_torch_reference(pkg, n, T, fused):
     ls = slice(T_.OFF["logstd"], T_.OFF["logstd"] + 15)
     torch.testing.assert_close(tr.grads[ls], g_ref[ls], rtol=1e-3, atol=1e-6)
     assert M == tr.M
+    # fp64 truth: no block, nor V / adv, further from it than 1.5 x the bf16 torch reference
+    R.fp64_pin(tr.grads, tr.V[0], tr.adv, tr.params.clone(), tr.obs_rm, tr.act, tr.logp, tr.rew, tr.done, n, T, cfg,
+               g_ref, info)
 
 
 @pytest.mark.parametrize("n,T,h1_recompute", [(256, 32, True), (96, 33, True), (256, 32, False), (96, 33, False)])

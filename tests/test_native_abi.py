@@ -84,6 +84,19 @@ def test_gnorm_partials_query_and_argument_checks(native):
     with pytest.raises(ValueError, match="2572 doubles"):  # checked before any launch
         native.call("dxrl_pg_fused_pair_gnorm", 0, C.byref(c), C.byref(a), 4096, 2571, C.byref(nb), None)
     fake = 1 << 20  # never dereferenced: the checks run first
+    # a batch of one 32-row chunk: the dW2 split counts would be capped to 1, so the call must fail
+    # before any launch (it failed only after overwriting dH2's partial slabs)
+    for x, net in ((c, 1), (a, 0)):
+        x.net, x.train, x.rows, x.grid, x.wgrad_splits, x.h1_mode = net, 1, 32, 256, 128, 0
+        for k in ("packed", "params", "obs", "act", "logp_old", "adv", "ret", "stats", "loss_partial", "grads"):
+            setattr(x, k, fake)
+    c.dh2, a.dh2, c.partial, a.partial, c.wgrad_partial, a.wgrad_partial = (fake + 4096 * i for i in range(1, 7))
+    with pytest.raises(ValueError, match="rows / 32"):
+        native.call("dxrl_pg_fused_pair_gnorm", 0, C.byref(c), C.byref(a), 4096, 2572, C.byref(nb), None)
+    c.rows = a.rows = 32 * 17
+    with pytest.raises(ValueError, match="wgrad_splits"):
+        c.wgrad_splits = 16
+        native.call("dxrl_pg_fused_pair_gnorm", 0, C.byref(c), C.byref(a), 4096, 2572, C.byref(nb), None)
     with pytest.raises(ValueError, match="padded parameter count"):
         native.call("dxrl_pg_adam_step", 0, *([fake] * 7), 12345, 3e-4, 0.9, 0.999, 1e-5, 1, 0.5, fake, 2572, fake,
                     fake, None)

@@ -57,3 +57,20 @@ def test_gae_matches_closed_form_single_episode():
     done[2] = 1  # episode boundary cuts the bootstrap and the trace
     adv2, _ = R.gae(rew, done, V, n, T, gamma, lam)
     assert abs(adv2[2] - (rew[2] - V[2])) < 1e-12
+
+
+def test_fp64_pin_ratios():
+    """pg_reference.fp64_pin: the bf16-emulating reference itself sits at ratio 1 of its own
+    distance to the fp64 truth; a result with doubled error (got = truth + 2 (ref - truth))
+    is rejected."""
+    import pytest
+    n, T = 8, 6
+    params, obs, act, logp_old, rew, done = make_case(n, T, dtype=torch.float32)
+    logp_old = logp_old.float()
+    g, info = R.loss_and_grads(params, obs, act, logp_old, rew, done, n, T, CFG, bf16=True)
+    r = R.fp64_pin(g, info["V"], info["adv"], params, obs, act, logp_old, rew, done, n, T, CFG, g, info)
+    assert all(abs(v - 1.0) < 1e-6 for v in r.values()), r
+    g64, info64 = R.loss_and_grads(params.double(), obs, act, logp_old, rew, done, n, T, CFG, bf16=False)
+    worse = g.double() + (g.double() - g64)
+    with pytest.raises(AssertionError):
+        R.fp64_pin(worse, info["V"], info["adv"], params, obs, act, logp_old, rew, done, n, T, CFG, g, info)

@@ -115,9 +115,12 @@ struct NoKHook {
 };
 // The first kD weight fragments of a fwd_tiles call, issuable ahead of the call (before the
 // barrier in front of its phase, so their L2 latency overlaps the barrier wait).
+#ifndef DXRL_WPF
+#define DXRL_WPF 8  // weight fragments issued ahead of a layer (before the barrier in front of it)
+#endif
 template <int KS>
 struct WPre {
-    static constexpr int kD = KS < 8 ? KS : 8;  // weight prefetch distance (k-steps)
+    static constexpr int kD = KS < DXRL_WPF ? KS : DXRL_WPF;  // weight prefetch distance (k-steps)
     bf16x8 wf[kD];
     const gbf16x8* wp;
 };
@@ -224,9 +227,10 @@ __device__ __forceinline__ void fwd_pipe_w(const bf16x8 (&wf)[KS], const bf16* A
         thook(q);  // caller work beside the last tile's epilogue (which has no MFMAs of its own)
     }
 }
-template <int KS, int kLda, int MT, typename Epi, typename Hook = NoHook, typename KHook = NoKHook>
+template <int KS, int kLda, int MT, typename Epi, typename Hook = NoHook, typename KHook = NoKHook,
+          typename THook = NoKHook>
 __device__ __forceinline__ void fwd_pipe(WPre<KS>& w, const bf16* A, int lane, Epi& epi, Hook hook = Hook{},
-                                         bool no_mfma = false, KHook khook = KHook{}) {
+                                         bool no_mfma = false, KHook khook = KHook{}, THook thook = THook{}) {
     constexpr int kD = WPre<KS>::kD;
     bf16x8 wf[KS];
 #pragma unroll
@@ -234,7 +238,7 @@ __device__ __forceinline__ void fwd_pipe(WPre<KS>& w, const bf16* A, int lane, E
 #pragma unroll
     for (int k = kD; k < KS; ++k) wf[k] = w.wp[64 * k];
     hook();  // loads the caller wants behind the last weight fragment (vmcnt retires in order)
-    fwd_pipe_w<KS, kLda, MT>(wf, A, lane, epi, no_mfma, khook);
+    fwd_pipe_w<KS, kLda, MT>(wf, A, lane, epi, no_mfma, khook, thook);
 }
 
 // fwd_pipe epilogues.  EpiTanh: tanh(acc + bias) -> bf16 H rows (store_hidden, pair by pair);
@@ -319,6 +323,14 @@ __device__ __forceinline__ void store_hidden(const f32x16 (&acc)[MT], int ft, co
         }
 }
 
+// (DXRL_GATE_PK: gate_in_place -- the dH2 gate, 4 MFMAs per tile beside it -- on packed f32)
+#ifndef DXRL_GATE_PK
+#define DXRL_GATE_PK 1
+#endif
+__device__ __forceinline__ f32x2 gate2_in_place(f32x2 g, f32x2 y) {
+    if constexpr (DXRL_GATE_PK != 0) return tanh_gate2_pk(g, y);
+    else return tanh_gate2(g, y);
+}
 // Y[m][f] <- bf16(acc[f][m] * (1 - Y[m][f]^2)) for this wave's features (tanh' gate, in place)
 template <int MT>
 __device__ __forceinline__ void gate_in_place(const f32x16 (&acc)[MT], int ft, bf16* Y, int lane) {
@@ -333,7 +345,7 @@ __device__ __forceinline__ void gate_in_place(const f32x16 (&acc)[MT], int ft, b
                 bf16x4 v;
 #pragma unroll
                 for (int u = 0; u < 4; u += 2) {
-                    const f32x2 t = tanh_gate2(f32x2{acc[mt][4 * g + u], acc[mt][4 * g + u + 1]},
+                    const f32x2 t = gate2_in_place(f32x2{acc[mt][4 * g + u], acc[mt][4 * g + u + 1]},
                                                f32x2{from_bf16(y[u]), from_bf16(y[u + 1])});
                     v[u] = to_bf16(t.x);
                     v[u + 1] = to_bf16(t.y);
@@ -417,14 +429,6 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #ifndef DXRL_FWD_EARLY_X
 #define DXRL_FWD_EARLY_X 1
 #endif
-// train passes: all 16 W2 fragments of the wave's feature tile issued at the start of L1 and all 16
-// W2T fragments at the start of the dW3 / dH2 phase (a phase ahead of their layer, held in
-// registers: L2 and dH1 then open with their whole weight slice on chip instead of streaming
-// half of it from L2 behind their first MFMAs)
-#ifndef DXRL_EARLY_W
-#define DXRL_EARLY_W 3  // bit 0: W2 under L1, bit 1: W2T under dW3 / dH2
-#endif
-
 // dW1 without the barrier after dH1: a wave's dW1 reads only its own dH1 columns (and X), so the
 // MFMAs of the first three 32-sample blocks issue beside dH1's last epilogue (VALU only) and the
 // db2 column sums' second stage moves behind the end-of-tile barrier
@@ -541,9 +545,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     // 160 KB of weight fragments from L2 per tile and workgroup
     constexpr bool kResW = !kTrain && kNT == 1 && DXRL_FWD_RESIDENT_W && DXRL_L2_PIPE;
     constexpr bool kEarlyX = kResW && DXRL_FWD_EARLY_X;
-    constexpr bool kDw1Tail = kTrain && kNT == 1 && kMT == 4 && DXRL_EARLY_W >= 2 && DXRL_DW1_TAIL && DXRL_DH2_IN_DH1;
-    constexpr bool kEarlyW = kTrain && kNT == 1 && (DXRL_EARLY_W & 1);
-    constexpr bool kEarlyWT = kTrain && kNT == 1 && (DXRL_EARLY_W & 2);
+    constexpr bool kDw1Tail = kTrain && kNT == 1 && kMT == 4 && DXRL_DW1_TAIL && DXRL_DH2_IN_DH1;
     bf16x8 w1res[kResW ? kIn / 16 : 1], w2res[kResW ? kH / 16 : 1];
     if constexpr (kResW) {
         const gbf16x8* p1 = (const gbf16x8*)p.W1 + (int64_t)ft0 * (kIn / 16) * 64 + lane;
@@ -627,13 +629,6 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // HBM load issued here would make every weight-fragment wait below wait for it too)
 
         // ---- L1, L2 (wave w: hidden features 64w .. 64w + 63, all 128 samples)
-        bf16x8 w2e[kEarlyW ? kH / 16 : 1];  // kEarlyW: this wave's W2 slice, in flight under L1
-        if constexpr (kEarlyW) {
-            const gbf16x8* wp = (const gbf16x8*)W2 + (int64_t)ft0 * (kH / 16) * 64 + lane;
-#pragma unroll
-            for (int k = 0; k < kH / 16; ++k) w2e[k] = wp[64 * k];
-            __builtin_amdgcn_sched_barrier(0);
-        }
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             // bias = W1 column 45 (X column 45 = 1)
@@ -643,7 +638,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         }
         // the first W2 fragments go out before the barrier (their L2 latency overlaps its wait)
         WPre<kH / 16> pw2;
-        if constexpr (!kResW && !kEarlyW) w_prefetch(pw2, W2, kH / 16, ft0, lane);
+        if constexpr (!kResW) w_prefetch(pw2, W2, kH / 16, ft0, lane);
         STAMP(2);
         __syncthreads();
         STAMP(3);
@@ -706,9 +701,6 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             if constexpr (kResW) {  // biases and head inputs resident: nothing to load
                 EpiTanh e2r{H2, 32 * (ft0 + j) + 4 * h, r, bkres};
                 fwd_pipe_w<kH / 16, kHp, kMT>(w2res, H1, lane, e2r, (diag & 32) != 0);
-            } else if constexpr (kEarlyW) {  // the W2 slice is in registers: the head inputs go out now
-                l2_hook();
-                fwd_pipe_w<kH / 16, kHp, kMT>(w2e, H1, lane, e2, (diag & 32) != 0);
             } else {
                 fwd_pipe<kH / 16, kHp, kMT>(pw2, H1, lane, e2, l2_hook, (diag & 32) != 0);
             }
@@ -1008,13 +1000,6 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         __syncthreads();
         STAMP(8);
 
-        bf16x8 w2te[kEarlyWT ? kH / 16 : 1];  // kEarlyWT: this wave's W2T slice, in flight under dW3 / dH2
-        if constexpr (kEarlyWT) {
-            const gbf16x8* wp = (const gbf16x8*)W2T + (int64_t)ft0 * (kH / 16) * 64 + lane;
-#pragma unroll
-            for (int k = 0; k < kH / 16; ++k) w2te[k] = wp[64 * k];
-            __builtin_amdgcn_sched_barrier(0);
-        }
         // ---- dW3 += dout^T H2 (wave w: H2 columns of its tiles), then dH2 in place of H2
 #pragma unroll
         for (int kk = 0; kk < kTR; kk += 32) {
@@ -1028,27 +1013,14 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         }
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
+            f32x16 acc[kMT];
             // dH2^T = W3^T dout^T over head rows 0..15 (dout rows 16..31 are zero)
-            if constexpr (kEarlyWT) {
-                // one 32-sample tile at a time (one accumulator live beside the W2T slice in flight;
-                // the same single MFMA per tile as fwd_run<1>, so the same bits)
-                const bf16* ap = D + r * kDp + 8 * h;
-#pragma unroll
-                for (int mt = 0; mt < kMT; ++mt) {
-                    f32x16 acc1[1];
-                    zero_acc(acc1[0]);
-                    acc1[0] = mfma32(pw3t.wf[0], *reinterpret_cast<const bf16x8*>(ap + 32 * mt * kDp), acc1[0]);
-                    gate_in_place(acc1, ft0 + j, H2 + 32 * mt * kHp, lane);
-                }
-            } else {
-                f32x16 acc[kMT];
-                if (j == 0) fwd_run<1, kDp, kMT>(pw3t, D, acc, lane);
-                else fwd_tiles<1, kDp, kMT>(W3T, kOut / 16, ft0 + j, D, acc, lane);
-                gate_in_place(acc, ft0 + j, H2, lane);
-            }
+            if (j == 0) fwd_run<1, kDp, kMT>(pw3t, D, acc, lane);
+            else fwd_tiles<1, kDp, kMT>(W3T, kOut / 16, ft0 + j, D, acc, lane);
+            gate_in_place(acc, ft0 + j, H2, lane);
         }
         WPre<kH / 16> pw2t;  // dH1's first W2T fragments, ahead of the barrier
-        if constexpr (!kEarlyWT) w_prefetch(pw2t, W2T, kH / 16, ft0, lane);
+        w_prefetch(pw2t, W2T, kH / 16, ft0, lane);
         STAMP(9);
         __syncthreads();
         STAMP(10);
@@ -1104,9 +1076,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                             if (!(diag & 4)) acc1[0][ri][ci] = mfma16(a, b[ci], acc1[0][ri][ci]);
                     }
                 };
-                fwd_pipe_w<kH / 16, kHp, kMT>(w2te, H2, lane, eg, false, copy_k, dw1_tail);
-            } else if constexpr (kEarlyWT) {
-                fwd_pipe_w<kH / 16, kHp, kMT>(w2te, H2, lane, eg, false, copy_k);
+                fwd_pipe<kH / 16, kHp, kMT>(pw2t, H2, lane, eg, NoHook{}, false, copy_k, dw1_tail);
             } else {
                 fwd_pipe<kH / 16, kHp, kMT>(pw2t, H2, lane, eg, NoHook{}, false, copy_k);
             }

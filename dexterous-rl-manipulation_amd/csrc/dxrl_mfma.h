@@ -139,14 +139,6 @@ __device__ __forceinline__ f32x2 tanh_gate2(f32x2 g, f32x2 y) {
     return f32x2{__builtin_fmaf(-(g.x * y.x), y.x, g.x), __builtin_fmaf(-(g.y * y.y), y.y, g.y)};
 }
 
-// The same gate as packed f32 (one v_pk_mul_f32 + one v_pk_fma_f32 for the pair): the same two
-// roundings per value, so the same bits.  Only where few MFMAs issue beside it (the packed forms
-// cost ~20 extra cycles each next to an MFMA: the dH2 gate, 4 MFMAs per 64 values)
-__device__ __forceinline__ f32x2 tanh_gate2_pk(f32x2 g, f32x2 y) {
-    const f32x2 gy = g * y;
-    return __builtin_elementwise_fma(-gy, y, g);
-}
-
 // tanh' gate of a back-propagated gradient: g (1 - y^2) as one multiply + one FMA
 __device__ __forceinline__ float tanh_gate(float g, float y) { return __builtin_fmaf(-(g * y), y, g); }
 

@@ -115,12 +115,11 @@ struct NoKHook {
 };
 // The first kD weight fragments of a fwd_tiles call, issuable ahead of the call (before the
 // barrier in front of its phase, so their L2 latency overlaps the barrier wait).
-#ifndef DXRL_WPF
-#define DXRL_WPF 8  // weight fragments issued ahead of a layer (before the barrier in front of it)
-#endif
 template <int KS>
 struct WPre {
-    static constexpr int kD = KS < DXRL_WPF ? KS : DXRL_WPF;  // weight prefetch distance (k-steps)
+    // weight prefetch distance (k-steps; 12 or 16, all of W2 issued ahead of the barrier in front
+    // of its layer, measured within 0.7 %: profiles/r06/ab_wpf_gatepk_rejected.log)
+    static constexpr int kD = KS < 8 ? KS : 8;
     bf16x8 wf[kD];
     const gbf16x8* wp;
 };
@@ -323,36 +322,41 @@ __device__ __forceinline__ void store_hidden(const f32x16 (&acc)[MT], int ft, co
         }
 }
 
-// (DXRL_GATE_PK: gate_in_place -- the dH2 gate, 4 MFMAs per tile beside it -- on packed f32)
-#ifndef DXRL_GATE_PK
-#define DXRL_GATE_PK 1
-#endif
-__device__ __forceinline__ f32x2 gate2_in_place(f32x2 g, f32x2 y) {
-    if constexpr (DXRL_GATE_PK != 0) return tanh_gate2_pk(g, y);
-    else return tanh_gate2(g, y);
-}
 // Y[m][f] <- bf16(acc[f][m] * (1 - Y[m][f]^2)) for this wave's features (tanh' gate, in place)
+// Y[m][f] <- bf16(acc[f][m] * (1 - Y[m][f]^2)) for this wave's features (tanh' gate, in place).
+// gate_load reads all 4 x MT Y pieces first (the caller issues it ahead of the MFMAs that make acc,
+// so one LDS latency hides under them; read one by one right before use, the compiler's schedule
+// waited out each read in turn: lgkmcnt(0) eight times per tile)
 template <int MT>
-__device__ __forceinline__ void gate_in_place(const f32x16 (&acc)[MT], int ft, bf16* Y, int lane) {
+__device__ __forceinline__ void gate_load(bf16x4 (&ys)[4][MT], int ft, const bf16* Y, int lane) {
     const int r = lane & 31, h = lane >> 5;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int f0 = 32 * ft + 8 * g + 4 * h;
+    for (int g = 0; g < 4; ++g)
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                bf16x4* yp = reinterpret_cast<bf16x4*>(Y + (32 * mt + r) * kHp + f0);
-                const bf16x4 y = *yp;
-                bf16x4 v;
+        for (int mt = 0; mt < MT; ++mt)
+            ys[g][mt] = *reinterpret_cast<const bf16x4*>(Y + (32 * mt + r) * kHp + 32 * ft + 8 * g + 4 * h);
+}
+template <int MT>
+__device__ __forceinline__ void gate_store(const f32x16 (&acc)[MT], const bf16x4 (&ys)[4][MT], int ft, bf16* Y,
+                                           int lane) {
+    const int r = lane & 31, h = lane >> 5;
 #pragma unroll
-                for (int u = 0; u < 4; u += 2) {
-                    const f32x2 t = gate2_in_place(f32x2{acc[mt][4 * g + u], acc[mt][4 * g + u + 1]},
-                                               f32x2{from_bf16(y[u]), from_bf16(y[u + 1])});
-                    v[u] = to_bf16(t.x);
-                    v[u + 1] = to_bf16(t.y);
-                }
-                *yp = v;
+    for (int g = 0; g < 4; ++g) {
+        const int f0 = 32 * ft + 8 * g + 4 * h;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const bf16x4 y = ys[g][mt];
+            bf16x4 v;
+#pragma unroll
+            for (int u = 0; u < 4; u += 2) {
+                const f32x2 t = tanh_gate2(f32x2{acc[mt][4 * g + u], acc[mt][4 * g + u + 1]},
+                                           f32x2{from_bf16(y[u]), from_bf16(y[u + 1])});
+                v[u] = to_bf16(t.x);
+                v[u + 1] = to_bf16(t.y);
             }
+            *reinterpret_cast<bf16x4*>(Y + (32 * mt + r) * kHp + f0) = v;
         }
+    }
 }
 
 // A [kTR][kH] bf16 tile of LDS (pitch kHp) -> rows m0.. of an HBM matrix (leading dimension ld),
@@ -1014,10 +1018,12 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
 #pragma unroll 1
         for (int j = 0; j < kNT; ++j) {
             f32x16 acc[kMT];
+            bf16x4 ys[4][kMT];
+            gate_load(ys, ft0 + j, H2, lane);
             // dH2^T = W3^T dout^T over head rows 0..15 (dout rows 16..31 are zero)
             if (j == 0) fwd_run<1, kDp, kMT>(pw3t, D, acc, lane);
             else fwd_tiles<1, kDp, kMT>(W3T, kOut / 16, ft0 + j, D, acc, lane);
-            gate_in_place(acc, ft0 + j, H2, lane);
+            gate_store(acc, ys, ft0 + j, H2, lane);
         }
         WPre<kH / 16> pw2t;  // dH1's first W2T fragments, ahead of the barrier
         w_prefetch(pw2t, W2T, kH / 16, ft0, lane);
@@ -1032,9 +1038,15 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             constexpr int kRows = kTR / kFW;
             float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);  // padding rows carry dH2 = 0 (their dout is 0)
             const bf16* hp = H2 + (kRows * wave) * kHp + 4 * lane;
+            // every row read before the first add (read and summed row by row, the compiler waited
+            // out each pair of reads in turn: eight LDS round trips per tile); same adds, same order
+            bf16x4 rv[kRows];
+#pragma unroll
+            for (int rr = 0; rr < kRows; ++rr) rv[rr] = *reinterpret_cast<const bf16x4*>(hp + rr * kHp);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int rr = 0; rr < kRows; ++rr) {
-                const bf16x4 v = *reinterpret_cast<const bf16x4*>(hp + rr * kHp);
+                const bf16x4 v = rv[rr];
                 cs.x += from_bf16(v[0]);
                 cs.y += from_bf16(v[1]);
                 cs.z += from_bf16(v[2]);
@@ -1051,12 +1063,24 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             // dH2 tile -> HBM (Y of the dW2 GEMM) in this phase's shadow: one 16-byte chunk per
             // thread every 8th step (the stores go out after every weight fragment, so no
             // fragment wait queues behind them; H2 holds dH2 read-only here)
+            // The chunks go out from the second sample tile on (k-step 16 + kEvery i): a store
+            // issued among the first tile's k-steps, while W2T fragments still stream in, made
+            // the compiler's vmcnt waits for them one fragment deeper (and the last one a full
+            // drain, the store's row guard being a branch).  Each chunk is read from LDS three
+            // steps ahead of its store (read right before it, its wait drained every LDS read in
+            // flight, the B-operand prefetch included).
+            bf16x8 cv;
             const auto copy_k = [&](int sidx) {
-                constexpr int kEvery = kMT * (kH / 16) / kCopyU;
-                if (diag & 1 || sidx % kEvery != kEvery - 1) return;
-                const int c = tid_l + kFThreads * (sidx / kEvery), row = c >> 5, col = 8 * (c & 31);
-                const bf16x8 v = *reinterpret_cast<const bf16x8*>(H2 + row * kHp + col);
-                if (m0 + row < p.rows) store_dh2(p.dh2_out + (m0 + row) * kH + col, v);
+                // (64-sample tiles: too few steps after the first tile; they start at step 3)
+                constexpr int kSteps = kMT * (kH / 16);
+                constexpr int kFirst = (kSteps - kH / 16) / kCopyU >= 4 ? kH / 16 : 2;
+                constexpr int kEvery = (kSteps - kFirst) / kCopyU, kAhead = kEvery >= 4 ? 3 : kEvery - 1;
+                static_assert(kAhead >= 1 && kFirst >= kAhead && kFirst + kEvery * kCopyU <= kSteps, "copy schedule");
+                if (diag & 1 || sidx < kFirst - kAhead) return;
+                const int i = (sidx - (kFirst - kAhead)) / kEvery, ph = (sidx - (kFirst - kAhead)) % kEvery;
+                const int c = tid_l + kFThreads * i, row = c >> 5, col = 8 * (c & 31);
+                if (ph == 0 && i < kCopyU) cv = *reinterpret_cast<const bf16x8*>(H2 + row * kHp + col);
+                if (ph == kAhead && i < kCopyU && m0 + row < p.rows) store_dh2(p.dh2_out + (m0 + row) * kH + col, cv);
             };
             if constexpr (kDw1Tail) {
                 // dW1 of sample blocks 0..2 (gated during the tile loop) beside the tail epilogue

@@ -1328,424 +1328,6 @@ __device__ __forceinline__ double sumsq4(float a, float b, float c, float d) {
     return (((double)a * a + (double)b * b) + (double)c * c) + (double)d * d;
 }
 
-// ---------------------------------------------------------------- two-tile train pass (round 6)
-// k_pg_dual<kNet>: the train pass of k_pg_fused<8, 128, true, kNet> as a two-tile software
-// pipeline.  The LDS holds two 64-sample tiles (two TileLds<64> slots of 80 KiB); the tile loop
-// runs in periods of three stages, each closed by a barrier, pairing a forward phase of tile k + 1
-// with a backward phase of tile k:
-//   stage 1  F1 = layer 1 of tile k + 1            | B1 = dW3 and the dH2 gate of tile k
-//   stage 2  F2 = layer 2 (+ head inputs) of k + 1 | B2 = db2 rows, dH1 (+ dH2 -> HBM) of tile k
-//   stage 3  F3 = the head of tile k + 1           | B3 = dW1 of tile k
-// (and one barrier for the X store of tile k + 1 at a period's start).  The two phases of a stage
-// touch different slots, so each wave runs both with no barrier between them -- and the two waves
-// of a SIMD run them in OPPOSITE orders (waves 0..3 forward first, waves 4..7 backward first), so
-// one's tanh-heavy forward phase issues beside the other's MFMA-heavy backward phase instead of
-// both running the same phase in lockstep (k_pg_fused's stamps: layer 1 VALU-issue-bound with the
-// matrix pipe idle, dH1 with it half used, profiles/r05/fused_stamps_r05.log).  Per sample the
-// MFMA chains, their k order and the epilogues are k_pg_fused's: H1, H2, the head outputs, dout,
-// dH2 (and so dW2) and dH1 are the same bits; dW1 / dW3 / db2 / the loss sums add the same terms
-// over a different tile set per workgroup (f32 order).  The head runs on waves 0..3 (16 samples
-// each, the 16x16x32 heads of k_pg_fused); db2 accumulates per wave row group across the launch.
-template <int kNet>
-__global__ __launch_bounds__(512, 1) void k_pg_dual(FusedArgs p) {
-    constexpr int kTR = 64, kFW = 8, kMT = kTR / 32, kFThreads = 64 * kFW;
-    constexpr bool kActor = kNet == 0;
-    constexpr int kCopyU = kTR * (kH / 8) / kFThreads;  // dH2 16-byte chunks per thread and tile
-    using L = TileLds<kTR>;
-    __shared__ __attribute__((aligned(16))) bf16 lds[2 * L::kElems];
-    const int tid = threadIdx.x, wave = tid >> 6;
-    // lane-derived values are re-derived at every stage (fence()): hoisted out of the tile loop,
-    // the addresses built from them for both slots would hold dozens of registers
-    int lane = tid & 63, r = lane & 31, h = lane >> 5;
-    const auto fence = [&]() { asm volatile("" : "+v"(lane), "+v"(r), "+v"(h)); };
-    const bool hi = __builtin_amdgcn_readfirstlane(wave) >= kFW / 2;  // the second wave of its SIMD
-    const bool headw = !hi;                                          // waves 0..3 run the heads
-#if DXRL_FUSED_PRIO
-    if (hi) __builtin_amdgcn_s_setprio(1);
-#endif
-    const int ft0 = wave;  // this wave's 32-wide feature tile
-    const int64_t ntiles = (p.rows + kTR - 1) / kTR;
-    const int64_t nmine = (int64_t)blockIdx.x < ntiles ? (ntiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-    const auto row0 = [&](int64_t k) { return ((int64_t)blockIdx.x + k * gridDim.x) * kTR; };
-    const auto Xs = [&](int s) { return lds + s * L::kElems + L::kOffX; };
-    const auto H1s = [&](int s) { return lds + s * L::kElems + L::kOffH1; };
-    const auto H2s = [&](int s) { return lds + s * L::kElems + L::kOffH2; };
-    const auto Ds = [&](int s) { return lds + s * L::kElems + L::kOffD; };
-
-    // launch-long accumulators (as k_pg_fused's, 16x16x32 tiles of the nonzero rows / columns)
-    f32x4 acc3[2], acc1[2][3];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        acc3[0][q] = acc3[1][q] = 0.0f;
-#pragma unroll
-        for (int ri = 0; ri < 2; ++ri)
-#pragma unroll
-            for (int ci = 0; ci < 3; ++ci) acc1[ri][ci][q] = 0.0f;
-    }
-    float dls[4], db3[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dls[i] = db3[i] = 0.0f;
-    float lsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    float4 cs2 = make_float4(0.f, 0.f, 0.f, 0.f);  // dL/db2: this wave's 8-row groups, columns 4 lane ..
-
-    const auto uniform_f64 = [](double v) {
-        const uint64_t u = __double_as_longlong(v);
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi_ = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
-        return __longlong_as_double((long long)(((uint64_t)hi_ << 32) | lo));
-    };
-    const double adv_mean = uniform_f64(kActor ? p.stats[2] : 0.0);
-    const double adv_inv = uniform_f64(kActor ? 1.0 / (p.stats[4] + 1e-8) : 1.0);
-    // resident for the launch: the layer-2 biases of this feature tile, the heads' constants
-    float bkres[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q)
-        bkres[q] = tanh_bias(((gf32*)p.b2)[(int64_t)(32 * ft0 + 8 * (q >> 2) + 4 * h + (q & 3)) * kHx]);
-    float b3res = 0.0f;
-    float ahls[4], ahb3[4];  // actor: log sigma and mu bias of head rows 4 (lane >> 4) .. + 3
-    if constexpr (!kActor) {
-        b3res = ((gf32*)p.b3)[0];
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int o = 4 * (lane >> 4) + i;
-            ahls[i] = o < kAct ? ((gf32*)p.logstd)[o] : 0.0f;
-            ahb3[i] = ((gf32*)p.b3)[(int64_t)o * kHx];
-        }
-    }
-
-    // X tile prefetch: 64 rows x 8 chunks of 16 B, one per thread
-    bf16x8 xr;
-    const auto fetch_x = [&](int64_t k) {
-        int t = tid;
-        asm volatile("" : "+v"(t));
-        const int row = t >> 3, col = 8 * (t & 7);
-        const int64_t m = row0(k) + row;
-        xr = m < p.rows ? *reinterpret_cast<const bf16x8*>(p.X + m * kIn + col) : zero8();
-    };
-    const auto store_x = [&](int s) {
-        const int row = tid >> 3, col = 8 * (tid & 7);
-        *reinterpret_cast<bf16x8*>(Xs(s) + row * kXp + col) = xr;
-    };
-    // head inputs of the tile in F2 -> F3 (head waves: sample 16 w + (lane & 15))
-    float hv = 0.0f, adv = 0.0f;
-    float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f);
-    bf16x8 w3h[8];  // the head's A fragments: mu rows lane & 15 (actor) / the value row (critic, row 0)
-    // (issued at the start of stage 3 ahead of the wave's dW1, consumed by its head after it)
-    const auto load_w3h = [&]() {
-        if constexpr (kActor) {
-            const bf16* W3rm = opaque(p.W3rm) + (lane & 15) * kHx + 8 * (lane >> 4);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) w3h[q] = *(const gbf16x8*)(W3rm + 32 * q);
-        } else {
-            const bf16* W3rm = opaque(p.W3rm) + 8 * (lane >> 4);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) w3h[q] = (lane & 15) == 0 ? *(const gbf16x8*)(W3rm + 32 * q) : zero8();
-        }
-    };
-
-    // ---- the six phases (s: LDS slot, k: the workgroup's tile index)
-    const auto F1 = [&](int s) {
-        WPre<kIn / 16> pw1;
-        w_prefetch(pw1, opaque(p.W1), kIn / 16, ft0, lane);
-        EpiTanh e1{H1s(s), 32 * ft0 + 4 * h, r, nullptr};
-        fwd_pipe<kIn / 16, kXp, kMT>(pw1, Xs(s), lane, e1);
-    };
-    const auto F2 = [&](int s, int64_t k) {
-        WPre<kH / 16> pw2;
-        w_prefetch(pw2, opaque(p.W2), kH / 16, ft0, lane);
-        const auto hook = [&]() {  // behind the last W2 fragment (vmcnt retires in issue order)
-            if (!headw) return;
-            const int64_t m16 = row0(k) + 16 * wave + (lane & 15), mc = m16 < p.rows ? m16 : p.rows - 1;
-            if constexpr (kActor) {
-                hv = p.logp_old[mc];
-                a0 = *reinterpret_cast<const float4*>(p.act + mc * kActPad + 4 * (lane >> 4));
-                adv = p.adv[mc];
-            } else {
-                hv = p.ret[mc];
-            }
-        };
-        EpiTanh e2{H2s(s), 32 * ft0 + 4 * h, r, bkres};
-        fwd_pipe<kH / 16, kHp, kMT>(pw2, H1s(s), lane, e2, hook);
-    };
-    const auto F3 = [&](int s, int64_t k) {
-        if (!headw) return;
-        const int s16 = 16 * wave + (lane & 15), g4 = lane >> 4;
-        const bf16* hb = H2s(s) + s16 * kHp + 8 * g4;
-        const int64_t m16 = row0(k) + s16;
-        bf16* D = Ds(s);
-        f32x4 a16 = {0.0f, 0.0f, 0.0f, 0.0f};
-        if constexpr (!kActor) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) a16 = mfma16(w3h[q], *reinterpret_cast<const bf16x8*>(hb + 32 * q), a16);
-            const bool v16 = m16 < p.rows && lane < 16;
-            float d0 = 0.0f;
-            if (v16) {
-                const float e = (a16[0] + b3res) - hv;  // hv: the return
-                d0 = from_bf16(to_bf16(p.vf2 * e * p.sc));
-                db3[0] += d0;
-                lsum[1] += e * e;
-            }
-            bf16x8 dv = zero8();
-            if (lane < 16) dv[0] = to_bf16(d0);
-            *reinterpret_cast<bf16x8*>(D + s16 * kDp + 8 * g4) = dv;
-        } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) a16 = mfma16(w3h[q], *reinterpret_cast<const bf16x8*>(hb + 32 * q), a16);
-            const bool v16 = m16 < p.rows;
-            float mu[4], a[4], iv2[4], t[4], d[4];
-            a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int o = 4 * g4 + i;
-                iv2[i] = __expf(-2.0f * ahls[i]);
-                mu[i] = a16[i] + ahb3[i];
-                const float z = (a[i] - mu[i]) * __expf(-ahls[i]);
-                t[i] = o < kAct ? -0.5f * z * z - ahls[i] - 0.5f * kLog2PiF : 0.0f;
-                d[i] = 0.0f;
-            }
-            // log pi(a|s): the sample's 15 terms gathered from its four lanes, summed in action order
-            float tt[16];
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) tt[4 * g + i] = __shfl(t[i], (lane & 15) + 16 * g);
-            float lp = 0.0f;
-#pragma unroll
-            for (int o = 0; o < kAct; ++o) lp += tt[o];
-            const float lo = hv;
-            const float ratio = __expf(lp - lo);
-            const float A = (float)(((double)adv - adv_mean) * adv_inv);
-            const float s1 = ratio * A;
-            const float rc = fminf(fmaxf(ratio, 1.0f - p.clip_eps), 1.0f + p.clip_eps);
-            const float s2 = rc * A;
-            float g = 0.0f;
-            if (s1 <= s2 || ratio == rc) g = -A * ratio;  // d(-min(s1, s2)) / d logp
-            g *= p.sc;
-            if (v16) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int o = 4 * g4 + i;
-                    if (o < kAct) {
-                        const float dd = a[i] - mu[i];
-                        d[i] = from_bf16(to_bf16(g * dd * iv2[i]));  // dlogp/dmu = (a - mu) / sigma^2
-                        dls[i] += g * (dd * dd * iv2[i] - 1.0f);       // dlogp/dlogstd
-                        db3[i] += d[i];
-                    }
-                }
-                if (g4 == 0) {
-                    lsum[0] += -fminf(s1, s2);
-                    lsum[2] += fabsf(ratio - 1.0f) > p.clip_eps ? 1.0f : 0.0f;
-                    lsum[3] += lo - lp;
-                }
-            }
-            bf16x4 dv, zv;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                dv[i] = to_bf16(d[i]);
-                zv[i] = (bf16)0.0f;
-            }
-            *reinterpret_cast<bf16x4*>(D + s16 * kDp + 4 * g4) = dv;        // head rows 4 g4 .. + 3
-            *reinterpret_cast<bf16x4*>(D + s16 * kDp + 16 + 4 * g4) = zv;   // rows 16 .. 31: zero
-        }
-    };
-    const auto B1 = [&](int s) {
-        WPre<1> pw3t;
-        w_prefetch(pw3t, opaque(p.W3T), kOut / 16, ft0, lane);
-        bf16x4 ys[4][kMT];
-        gate_load(ys, ft0, H2s(s), lane);
-        // dW3 += dout^T H2 (this wave's H2 columns), then dH2 = (dout W3) * (1 - H2^2) in place
-#pragma unroll
-        for (int kk = 0; kk < kTR; kk += 32) {
-            const bf16x8 a = wg_frag<kDp>(Ds(s), 0, kk, lane);
-#pragma unroll
-            for (int ci = 0; ci < 2; ++ci) acc3[ci] = mfma16(a, wg_frag<kHp>(H2s(s), 32 * ft0 + 16 * ci, kk, lane), acc3[ci]);
-        }
-        f32x16 acc[kMT];
-        fwd_run<1, kDp, kMT>(pw3t, Ds(s), acc, lane);
-        gate_store(acc, ys, ft0, H2s(s), lane);
-    };
-    const auto B2 = [&](int s, int64_t k) {
-        WPre<kH / 16> pw2t;
-        w_prefetch(pw2t, opaque(p.W2T), kH / 16, ft0, lane);
-        {  // db2: this wave's rows 8 w .. 8 w + 7, columns 4 lane .. (padding rows carry dH2 = 0)
-            constexpr int kRows = kTR / kFW;
-            const bf16* hp = H2s(s) + (kRows * wave) * kHp + 4 * lane;
-            bf16x4 rv[kRows];
-#pragma unroll
-            for (int rr = 0; rr < kRows; ++rr) rv[rr] = *reinterpret_cast<const bf16x4*>(hp + rr * kHp);
-#pragma unroll
-            for (int rr = 0; rr < kRows; ++rr) {
-                cs2.x += from_bf16(rv[rr][0]);
-                cs2.y += from_bf16(rv[rr][1]);
-                cs2.z += from_bf16(rv[rr][2]);
-                cs2.w += from_bf16(rv[rr][3]);
-            }
-        }
-        const int64_t m0 = row0(k);
-        bf16* H2 = H2s(s);
-        bf16x8 cv;
-        // dH2 -> HBM from the second sample tile on, each chunk read three steps ahead (k_pg_fused)
-        const auto copy_k = [&](int sidx) {
-            constexpr int kSteps = kMT * (kH / 16), kFirst = kH / 16;
-            constexpr int kEvery = (kSteps - kFirst) / kCopyU, kAhead = 3;
-            static_assert(kEvery > kAhead && kFirst + kEvery * kCopyU <= kSteps, "copy schedule");
-            if (sidx < kFirst - kAhead) return;
-            const int i = (sidx - (kFirst - kAhead)) / kEvery, ph = (sidx - (kFirst - kAhead)) % kEvery;
-            int t = tid;
-            asm volatile("" : "+v"(t));
-            const int c = t + kFThreads * i, row = c >> 5, col = 8 * (c & 31);
-            if (ph == 0 && i < kCopyU) cv = *reinterpret_cast<const bf16x8*>(H2 + row * kHp + col);
-            if (ph == kAhead && i < kCopyU && m0 + row < p.rows) store_dh2(p.dh2_out + (m0 + row) * kH + col, cv);
-        };
-        EpiGate eg{H1s(s), 32 * ft0 + 4 * h, r};
-        fwd_pipe<kH / 16, kHp, kMT>(pw2t, H2, lane, eg, NoHook{}, false, copy_k);
-    };
-    const auto B3 = [&](int s) {
-#pragma unroll
-        for (int kk = 0; kk < kTR; kk += 32) {
-            bf16x8 b[3];
-#pragma unroll
-            for (int ci = 0; ci < 3; ++ci) b[ci] = wg_frag<kXp>(Xs(s), 16 * ci, kk, lane);
-#pragma unroll
-            for (int ri = 0; ri < 2; ++ri) {
-                const bf16x8 a = wg_frag<kHp>(H1s(s), 32 * ft0 + 16 * ri, kk, lane);
-#pragma unroll
-                for (int ci = 0; ci < 3; ++ci) acc1[ri][ci] = mfma16(a, b[ci], acc1[ri][ci]);
-            }
-        }
-    };
-
-    // ---- the pipeline: prologue (tile 0 forward), then one period per tile (its backward beside
-    //      the next tile's forward; the waves of a SIMD in opposite phase orders)
-    if (nmine > 0) {
-        fetch_x(0);
-        store_x(0);
-        if (nmine > 1) fetch_x(1);
-        __syncthreads();
-        F1(0);
-        __syncthreads();
-        F2(0, 0);
-        __syncthreads();
-        if (headw) load_w3h();
-        F3(0, 0);
-        __syncthreads();
-    }
-#pragma unroll 1
-    for (int64_t k = 0; k < nmine; ++k) {
-        const int s = (int)(k & 1), sn = s ^ 1;
-        const bool nx = k + 1 < nmine;
-        if (nx) {
-            store_x(sn);  // slot sn's previous tile (k - 1) finished its dW1 before the last barrier
-            if (k + 2 < nmine) fetch_x(k + 2);
-        }
-        __syncthreads();
-        fence();
-#pragma unroll 1
-        for (int o = 0; o < 2; ++o) {
-            if ((o == 0) != hi) {
-                if (nx) F1(sn);
-            } else {
-                B1(s);
-            }
-        }
-        __syncthreads();
-        fence();
-#pragma unroll 1
-        for (int o = 0; o < 2; ++o) {
-            if ((o == 0) != hi) {
-                if (nx) F2(sn, k + 1);
-            } else {
-                B2(s, k);
-            }
-        }
-        __syncthreads();
-        // stage 3: every wave's dW1; the head waves then run the next tile's head, its weight
-        // fragments issued ahead of the dW1 MFMAs
-        fence();
-        if (nx && headw) load_w3h();
-        B3(s);
-        if (nx) F3(sn, k + 1);
-        __syncthreads();
-    }
-
-    fence();
-    // ---- workgroup partials (k_pg_fused's layout; summed in a fixed order by the reductions)
-    float* part = p.part + (int64_t)blockIdx.x * kPartSize;
-    {
-        const int c16 = lane & 15, g16 = lane >> 4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int o = 4 * g16 + i;
-#pragma unroll
-            for (int ci = 0; ci < 2; ++ci) part[kPartW3 + o * kPW3C + 32 * ft0 + 16 * ci + c16] = acc3[ci][i];
-#pragma unroll
-            for (int ri = 0; ri < 2; ++ri) {
-                float* row = part + kPartW1 + (32 * ft0 + 16 * ri + o) * kPW1C;
-#pragma unroll
-                for (int ci = 0; ci < 3; ++ci) row[16 * ci + c16] = acc1[ri][ci][i];
-            }
-        }
-    }
-    // db2: the eight row groups of column c summed in wave order
-    float4* red4 = reinterpret_cast<float4*>(lds);
-    red4[wave * 64 + lane] = cs2;
-    __syncthreads();
-    if (tid < kH) {
-        const float* cs = reinterpret_cast<const float*>(lds);
-        float db2 = 0.0f;
-#pragma unroll
-        for (int w = 0; w < kFW; ++w) db2 += cs[w * kH + tid];
-        part[kPartB2 + tid] = db2;
-    }
-    __syncthreads();
-    // head sums: head rows o = 4 g + i of lanes 16 g .. + 15 of every (head) wave in (wave, lane)
-    // order, the loss terms over every lane in thread order (waves 4..7 hold zeros)
-    float* red = reinterpret_cast<float*>(lds);                  // [512][8]: dls[0..3], db3[0..3]
-    double* lred = reinterpret_cast<double*>(lds + 8192);       // [512][4], past red
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        red[tid * 8 + i] = dls[i];
-        red[tid * 8 + 4 + i] = db3[i];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) lred[tid * 4 + k] = (double)lsum[k];
-    __syncthreads();
-    if (tid < 32) {
-        const int o = tid, g = (o >> 2) & 3, i = o & 3;
-        float sl = 0.0f, sb = 0.0f;
-        if (o < 16) {
-            for (int w = 0; w < kFW; ++w)
-                for (int rr = 0; rr < 16; ++rr) {
-                    const int t = 64 * w + 16 * g + rr;
-                    sl += red[t * 8 + i];
-                    sb += red[t * 8 + 4 + i];
-                }
-            if (!kActor) {  // value head: row 0 only, register 0 of lanes 0..15 (k_pg_fused's critic sums)
-                sb = 0.0f;
-                if (o == 0)
-                    for (int w = 0; w < kFW; ++w)
-                        for (int rr = 0; rr < 16; ++rr) sb += red[(64 * w + rr) * 8 + 4];
-                sl = 0.0f;
-            }
-            part[kPartW3 + o * kPW3C + kH] = sb;  // bias column of the head
-            part[kPartLs + o] = sl;
-        }
-    } else if (tid < 36) {
-        const int k = tid - 32;
-        if (kActor ? k != 1 : k == 1) {
-            double sum = 0.0;
-            if (kActor) {
-                for (int t = 0; t < kFThreads; ++t) sum += lred[t * 4 + k];
-            } else {
-                for (int w = 0; w < kFW; ++w)
-                    for (int rr = 0; rr < 16; ++rr) sum += lred[(64 * w + rr) * 4 + 1];
-            }
-            p.loss[(int64_t)blockIdx.x * 4 + k] = sum;
-            for (int rw = blockIdx.x + gridDim.x; rw < p.loss_rows; rw += gridDim.x) p.loss[(int64_t)rw * 4 + k] = 0.0;
-        }
-    }
-}
-
 // Critic values (the forward-only pass) as its own kernel, pipelined across tiles: the layer-by-layer
 // instantiation k_pg_fused<8, 128, false, 1> closes four barriers per tile (X stored, L1 -> L2,
 // L2 -> head, end of tile).  Here the next tile's X is stored while L2 runs (X is free once L1 is
@@ -2212,19 +1794,6 @@ int fused_kernel(const dxrl_pg_fused_args* a, hipStream_t st, int* grid_out) {
     if ((diag & 8) && !stamps) (void)hipMalloc(&stamps, (size_t)65536 * 8 * 16 * 8);
     f.stamps = stamps;
     const bool dg = diag != 0;
-    // the two-tile pipelined train pass (k_pg_dual; DXRL_FUSED_DUAL=0 selects k_pg_fused, read per call)
-    const char* dv = getenv("DXRL_FUSED_DUAL");
-    const bool dual = train && tile == 128 && !dg && f.h1_out == nullptr && dv && atoi(dv) == 1;
-    if (dual) {
-        const int64_t nt64 = (a->rows + 63) / 64;
-        int64_t gd = a->grid < cus ? a->grid : cus;
-        if (nt64 < gd) gd = nt64;
-        if (c) hipLaunchKernelGGL(k_pg_dual<1>, dim3((unsigned)gd), dim3(512), 0, st, f);
-        else hipLaunchKernelGGL(k_pg_dual<0>, dim3((unsigned)gd), dim3(512), 0, st, f);
-        if (int rc = launch_check("k_pg_dual")) return rc;
-        *grid_out = (int)gd;
-        return DXRL_OK;
-    }
     if (tile == 64) {  // A/B geometry: the diagnostic instantiations only
         if (!train) hipLaunchKernelGGL((k_pg_fused<4, 64, false, 1, true>), dim3(grid), dim3(256), 0, st, f);
         else if (!c) hipLaunchKernelGGL((k_pg_fused<4, 64, true, 0, true>), dim3(grid), dim3(256), 0, st, f);

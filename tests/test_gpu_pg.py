@@ -216,48 +216,6 @@ def test_paired_learner_equals_two_passes(pkg, n, T, mb):
         assert torch.equal(la, lb)
 
 
-@pytest.mark.parametrize("n,T,mb", [(4096, 32, 1), (773, 32, 1), (2048, 32, 4), (5, 32, 1), (4096, 64, 1)])
-def test_two_tile_pass_equals_single_tile_pass(pkg, monkeypatch, n, T, mb):
-    """k_pg_dual (the two-tile pipelined train pass, the default) against k_pg_fused
-    (DXRL_FUSED_DUAL=0) on the same tapes: dH2 -- and with it dW2 -- bit for bit (same MFMA
-    chains and epilogues per sample), the loss sums and every other gradient block to f32
-    summation order (a different tile set per workgroup; 64-sample tiles, ragged last tiles,
-    a tile count below the grid, PPO minibatch slices)."""
-    outs = []
-    for dual in ("1", "0"):
-        monkeypatch.setenv("DXRL_FUSED_DUAL", dual)
-        _, tr = make(pkg, n, T, minibatches=mb)
-        tr.rollout()
-        tr.critic_values()
-        tr.advantages()
-        b = tr.minibatch_bounds()
-        got = []
-        for k in range(mb):
-            tr._mb = (b[k], b[k + 1] - b[k])
-            tr.train_passes()
-            torch.cuda.synchronize()
-            rows = b[k + 1] - b[k]
-            dh2 = [t[:rows].clone() for t in (tr.dH2, tr.dH2c) if t is not None]
-            got.append((tr.grads.clone(), tr.fused_loss.sum(0).clone(), dh2, rows))
-        outs.append(got)
-    T_ = pkg.trainer
-    for (ga, la, da, rows), (gb, lb, db, _) in zip(*outs):
-        for x, y in zip(da, db):
-            assert torch.equal(x, y)
-        for name in ("W2a", "W2c"):  # dW2 = dH2^T H1: the same dH2, the same contraction
-            blk = slice(T_.OFF[name], T_.OFF[name] + 256 * 288)
-            gx, gy = ga[blk].view(256, 288)[:, :256], gb[blk].view(256, 288)[:, :256]
-            assert torch.equal(gx, gy), name
-        for name in ("W1a", "W3a", "W1c", "W3c", "W2a", "W2c"):  # (W2: its bias column, db2)
-            x, y = tr.block(name, ga), tr.block(name, gb)
-            assert (x - y).norm() <= 1e-5 * y.norm() + 1e-12, name
-        ls = slice(T_.OFF["logstd"], T_.OFF["logstd"] + 15)
-        assert (ga[ls] - gb[ls]).norm() <= 1e-5 * gb[ls].norm() + 1e-12
-        # loss sums of O(1) per-sample terms; the policy term cancels to ~0 over normalised
-        # advantages, so its f32 order error is bounded per sample, not relative to the sum
-        torch.testing.assert_close(la, lb, rtol=1e-5, atol=2e-9 * rows)
-
-
 @pytest.mark.parametrize("n,T,mb,max_norm", [(256, 32, 1, 0.5), (2048, 32, 4, 1e-3), (512, 32, 1, 1e6)])
 def test_reduction_gnorm_partials_match_sumsq_path(pkg, n, T, mb, max_norm):
     """One rank, paired step (TrainerConfig.fused_gnorm): the grad-norm partials written by the

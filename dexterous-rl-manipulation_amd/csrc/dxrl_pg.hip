@@ -1124,16 +1124,14 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(const float* __restrict__ r
     if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
-// k_gae_lds: the same per-env recurrence, bit for bit (k_gae's expressions in k_gae's order), with
-// everything but the recurrence itself taken off the serial chain.  A 256-thread workgroup owns
-// 16 envs:
+// k_gae_lds: the same per-env recurrence (k_gae's expressions), with everything but the
+// recurrence itself taken off the serial chain and the recurrence itself a 16-lane wavefront
+// prefix per env (round 6, step 2 below).  A 256-thread workgroup owns 16 envs:
 //   1. all 256 threads load the envs' whole horizon (rew, V_t, V_{t+1}, done; batches of
 //      independent loads) and write delta_t = r_t + gamma V_{t+1} (1 - d_t) - V_t and the chain
 //      coefficient c_t = (gamma lambda)(1 - d_t) (selected from the done byte) into env-major LDS
 //      rows, zero-padded to a multiple of 8 steps;
-//   2. one lane per env runs A_t = delta_t + c_t A_{t+1} down its rows, 8 steps per chunk, the
-//      next chunk's operands read as four 16-byte loads while this one's chain runs (one multiply
-//      and one add per step on the chain);
+//   2. A_t = delta_t + c_t A_{t+1} down the rows as a segmented scan (16 lanes per env, below);
 //   3. all 256 threads write adv / ret back coalesced and accumulate the moments.
 // The padded steps run first, on zeros: A stays +0, which the chain starts from anyway.
 // Round 5: the chain read its operands as 16 scalar loads (delta, done byte) per 8 steps from
@@ -1214,36 +1212,57 @@ __global__ __launch_bounds__(kGlThreads) void k_gae_lds(const float* __restrict_
         Ce[e * P + t] = 0.0f;
     }
     __syncthreads();
-    // 2. the recurrence: lane e walks its rows down, chunk k = steps 8k .. 8k + 7
-    if (!(DXRL_GAE_DIAG & 1) && tid < kGlEnvs) {
-        const int e = tid;
+    // 2. the recurrence A_t = delta_t + c_t A_{t+1} as a wavefront prefix: 16 lanes per env (one
+    //    wave holds 4 envs), lane s owns the 8-step chunks [s nc / 16, (s + 1) nc / 16) of its env's
+    //    nc = T8 / 8 chunks.  (a) each lane composes its segment into the affine map A_start =
+    //    D + C A_in (D = the segment's recurrence from A_in = 0, C = the product of its c_t); (b) a
+    //    Hillis-Steele suffix scan over the 16 lanes (offsets 1, 2, 4, 8: map_s <- map_s o map_{s+off})
+    //    gives each lane A at the start of its segment, and lane s + 1's value is lane s's A_in;
+    //    (c) each lane reruns its segment's recurrence from A_in, storing A_t.  The chain is
+    //    2 (nc / 16) chunks + 4 scan steps long instead of nc chunks; inside a segment every A_t is
+    //    the sequential expression, the segment boundaries' A_in carry the composition's rounding
+    //    (pg_reference.gae restates this exact order).  Against one lane per env running the
+    //    whole chain (round 5): advantages phase 16.0-16.7 -> 13.1-14.0 us
+    //    (profiles/r06/ab_gae_scan.log).
+    if (!(DXRL_GAE_DIAG & 1)) {
+        const int e = tid >> 4, sg = tid & 15;
+        const int nc = T8 / 8, c_lo = sg * nc / 16, c_hi = (sg + 1) * nc / 16;
         const float4* L4 = reinterpret_cast<const float4*>(Le + e * P);
         const float4* C4 = reinterpret_cast<const float4*>(Ce + e * P);
-        float next_adv = 0.0f;
-        int k = T8 / 8 - 1;
-        float4 l0 = L4[2 * k], l1 = L4[2 * k + 1], c0 = C4[2 * k], c1 = C4[2 * k + 1];
-        for (; k >= 0; --k) {
-            const int kn = k > 0 ? k - 1 : 0;  // the next chunk's operands (a reload of chunk 0 at the end)
-            const float4 nl0 = L4[2 * kn], nl1 = L4[2 * kn + 1], nc0 = C4[2 * kn], nc1 = C4[2 * kn + 1];
-            __builtin_amdgcn_sched_barrier(0);  // the loads stay ahead of the chain (the scheduler sank them)
+        float D = 0.0f, C = 1.0f;
+        for (int k = c_hi - 1; k >= c_lo; --k) {
+            const float4 l0 = L4[2 * k], l1 = L4[2 * k + 1], q0 = C4[2 * k], q1 = C4[2 * k + 1];
             const float lq[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
-            const float cq[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+            const float cq[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+            for (int j = 7; j >= 0; --j) {
+                D = lq[j] + cq[j] * D;
+                C = cq[j] * C;
+            }
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const float Dn = __shfl_down(D, off, 16), Cn = __shfl_down(C, off, 16);
+            if (sg + off < 16) {
+                D = D + C * Dn;
+                C = C * Cn;
+            }
+        }
+        const float Dnext = __shfl_down(D, 1, 16);
+        float next_adv = sg == 15 ? 0.0f : Dnext;
+        for (int k = c_hi - 1; k >= c_lo; --k) {
+            const float4 l0 = L4[2 * k], l1 = L4[2 * k + 1], q0 = C4[2 * k], q1 = C4[2 * k + 1];
+            const float lq[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+            const float cq[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
             float aq[8];
 #pragma unroll
             for (int j = 7; j >= 0; --j) {
                 aq[j] = lq[j] + cq[j] * next_adv;
                 next_adv = aq[j];
             }
-            // the chunk's 8 advantages as two 16-byte stores (8 scalar stores each held the chain
-            // for the store's register read; no branch: padded steps land past T)
             float4* A4 = reinterpret_cast<float4*>(Ae + e * P + 8 * k);
             A4[0] = make_float4(aq[0], aq[1], aq[2], aq[3]);
             A4[1] = make_float4(aq[4], aq[5], aq[6], aq[7]);
-            __builtin_amdgcn_sched_barrier(0);
-            l0 = nl0;
-            l1 = nl1;
-            c0 = nc0;
-            c1 = nc1;
         }
     }
     __syncthreads();

@@ -48,8 +48,23 @@ def mlp_forward(X, Wd, net, bf16):
     return H1, H2, head
 
 
-def gae(rew, done, V, n, T, gamma, lam):
-    """rew/done [T*n], V [(T+1)*n] -> adv, ret [T*n] (f32 scan, the kernel's formula order)."""
+def gae_uses_segmented_scan(T):
+    """dxrl_pg_gae's kernel choice (csrc/dxrl_pg.hip): k_gae_lds (segmented scan) while the horizon's
+    LDS staging fits 152 KiB, else k_gae (one sequential chain per env)."""
+    pitch = (T + 7) // 8 * 8 + 4
+    return 16 * (12 * pitch + 4 * T) <= 152 * 1024
+
+
+def gae(rew, done, V, n, T, gamma, lam, scan=None):
+    """rew/done [T*n], V [(T+1)*n] -> adv, ret [T*n] (f32, the kernel's formula order).
+    scan (default: the kernel's choice for T): k_gae_lds's segmented wavefront scan -- the horizon
+    padded to 8-step chunks, 16 segments of whole chunks per env composed into affine maps, a
+    Hillis-Steele suffix scan over the segments, each segment rerun from its incoming value --
+    restated op for op; else the one-chain sequential recurrence of k_gae."""
+    if scan is None:
+        scan = gae_uses_segmented_scan(T)
+    if scan:
+        return _gae_segmented(rew, done, V, n, T, gamma, lam)
     rew, done, V = rew.view(T, n), done.view(T, n).float(), V.view(T + 1, n)
     adv = torch.empty(T, n, dtype=rew.dtype, device=rew.device)
     next_adv = torch.zeros(n, dtype=rew.dtype, device=rew.device)
@@ -63,6 +78,40 @@ def gae(rew, done, V, n, T, gamma, lam):
         adv[t] = a
         next_adv = a
         next_v = V[t]
+    ret = adv + V[:T]
+    return adv.reshape(-1), ret.reshape(-1)
+
+
+def _gae_segmented(rew, done, V, n, T, gamma, lam):
+    rew, done, V = rew.view(T, n), done.view(T, n).float(), V.view(T + 1, n)
+    dt, dev = rew.dtype, rew.device
+    g = torch.tensor(gamma, dtype=dt)
+    gl = g * torch.tensor(lam, dtype=dt)
+    T8 = (T + 7) // 8 * 8
+    delta = torch.zeros(T8, n, dtype=dt, device=dev)
+    c = torch.zeros(T8, n, dtype=dt, device=dev)
+    delta[:T] = rew + g * V[1:] * (1.0 - done) - V[:T]
+    c[:T] = torch.where(done > 0, torch.zeros((), dtype=dt, device=dev), gl.to(dev))
+    nc, S = T8 // 8, 16
+    seg = [(8 * (s * nc // S), 8 * ((s + 1) * nc // S)) for s in range(S)]
+    D = [torch.zeros(n, dtype=dt, device=dev) for _ in range(S)]
+    C = [torch.ones(n, dtype=dt, device=dev) for _ in range(S)]
+    for s, (lo, hi) in enumerate(seg):  # each segment's affine map from A_in = 0
+        for t in range(hi - 1, lo - 1, -1):
+            D[s] = delta[t] + c[t] * D[s]
+            C[s] = c[t] * C[s]
+    off = 1
+    while off < S:  # suffix scan, every lane reading its neighbour's value of the previous step
+        D, C = ([D[s] + C[s] * D[s + off] if s + off < S else D[s] for s in range(S)],
+                [C[s] * C[s + off] if s + off < S else C[s] for s in range(S)])
+        off *= 2
+    adv = torch.empty(T8, n, dtype=dt, device=dev)
+    for s, (lo, hi) in enumerate(seg):
+        a = D[s + 1] if s + 1 < S else torch.zeros(n, dtype=dt, device=dev)
+        for t in range(hi - 1, lo - 1, -1):
+            a = delta[t] + c[t] * a
+            adv[t] = a
+    adv = adv[:T]
     ret = adv + V[:T]
     return adv.reshape(-1), ret.reshape(-1)
 

@@ -582,9 +582,10 @@ def test_optimizer_step_matches_torch_clip_and_adam(pkg):
                                         # past the LDS staging limit: the k_gae fallback
                                         (200, 800, 0.01)])
 def test_gae_lds_scan_matches_sequential_reference(pkg, n, T, p_done):
-    """dxrl_pg_gae (k_gae_lds: the horizon staged in LDS by the whole workgroup, one lane per env
-    running the recurrence; k_gae past T = 600) gives pg_reference.gae's adv / ret (the kernel's
-    op order) bit for bit, and the moments (count, mean, M2) a two-pass f64 reduction's to 1e-9.
+    """dxrl_pg_gae (k_gae_lds: the horizon staged in LDS by the whole workgroup, the recurrence a
+    16-lane segmented wavefront scan per env; k_gae, one sequential chain per env, past T = 600)
+    gives pg_reference.gae's adv / ret (the restatement of the kernel's op order, scan included)
+    bit for bit, and the moments (count, mean, M2) a two-pass f64 reduction's to 1e-9.
     Ragged env counts, no dones and dense dones, horizons from 1 to 800.  `partial` is sized by
     dxrl_pg_gae_partial_doubles exactly, with a NaN canary block behind it that must survive
     (one Moments triple per workgroup; the header once documented half of that)."""

@@ -1,5 +1,6 @@
 """CPU: the manual PG backward (pg_reference.py, mirrored by the HIP kernels)
 equals torch autograd on the same PPO + value + entropy objective (fp64)."""
+import pytest
 import torch
 
 import pg_reference as R
@@ -57,6 +58,27 @@ def test_gae_matches_closed_form_single_episode():
     done[2] = 1  # episode boundary cuts the bootstrap and the trace
     adv2, _ = R.gae(rew, done, V, n, T, gamma, lam)
     assert abs(adv2[2] - (rew[2] - V[2])) < 1e-12
+
+
+@pytest.mark.parametrize("n,T,p_done", [(7, 1, 0.0), (5, 9, 0.2), (33, 200, 0.02), (4, 129, 0.0), (3, 600, 0.05)])
+def test_gae_segmented_scan_equals_sequential_recurrence(n, T, p_done):
+    """k_gae_lds's segmented scan (restated op for op by pg_reference.gae) against the one-chain
+    f32 recurrence and an f64 one: the composition only re-rounds each segment's incoming value, so
+    the two f32 forms agree to a few ulp of the chain's magnitude and both sit within 1e-5 of f64
+    (north star: returns within 1e-5)."""
+    g = torch.Generator().manual_seed(1000 * n + T)
+    rew = torch.randn(T * n, generator=g)
+    V = torch.randn((T + 1) * n, generator=g) * 3.0
+    done = (torch.rand(T * n, generator=g) < p_done).to(torch.uint8)
+    a_scan, r_scan = R.gae(rew, done, V, n, T, 0.99, 0.95, scan=True)
+    a_seq, r_seq = R.gae(rew, done, V, n, T, 0.99, 0.95, scan=False)
+    a64, _ = R.gae(rew.double(), done, V.double(), n, T, 0.99, 0.95, scan=False)
+    scale = a64.abs().max().item() + 1.0
+    assert (a_scan.double() - a_seq.double()).abs().max().item() <= 1e-6 * scale
+    assert (a_scan.double() - a64).abs().max().item() <= 1e-5 * scale
+    torch.testing.assert_close(r_scan, a_scan + V.view(T + 1, n)[:T].reshape(-1), rtol=0, atol=0)
+    if T <= 8:  # one chunk: a single segment holds the whole horizon, no composition at all
+        assert torch.equal(a_scan, a_seq)
 
 
 def test_fp64_pin_ratios():

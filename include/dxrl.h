@@ -308,13 +308,16 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
  * stats[0..4] as dxrl_pg_adv_combine(stats + 5, world = 1) would (single rank: no second call)
  * (per-env sums about the env's own first value, merged with Chan et al.'s pairwise update
  * in a fixed order: no sum(a^2) - mean sum(a) cancellation).
- * The scan is the SEQUENTIAL recurrence A_t = delta_t + (gamma lambda)(1 - d_t) A_{t+1} per env,
- * bit-exact against a one-env-at-a-time reverse loop in that operation order:
+ * The recurrence is A_t = delta_t + (gamma lambda)(1 - d_t) A_{t+1} per env:
  *   T <= 600 (~256 B per step in LDS, <= 152 KiB): k_gae_lds -- a 256-thread workgroup per 16
  *     envs stages the horizon in LDS with all its threads (delta_t and the chain coefficient
- *     computed in parallel), one lane per env runs the two-op chain, all threads store adv / ret;
- *     ceil(N / 16) workgroups;
- *   longer horizons: k_gae -- one thread per env, 64-env workgroups;  ceil(N / 64) workgroups.
+ *     computed in parallel), runs the recurrence as a wavefront-prefix scan (16 lanes per env:
+ *     each lane's segment of 8-step chunks composed into an affine map, a suffix scan of the maps
+ *     across the 16 lanes, each segment rerun from its incoming value), all threads store
+ *     adv / ret; ceil(N / 16) workgroups.  Bit-exact against tests/pg_reference.py's restatement
+ *     of that order; within ~1e-6 of the values' scale of the one-chain loop;
+ *   longer horizons: k_gae -- one thread per env running the sequential loop, 64-env workgroups;
+ *     ceil(N / 64) workgroups.
  * Each workgroup writes one (count, mean, M2) triple into `partial`.
  * partial: f64 [dxrl_pg_gae_partial_doubles(N, T)] (= 3 ceil(N / 16), enough for either kernel);
  * stats: f64 [8]. */

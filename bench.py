@@ -87,6 +87,9 @@ def parse():
     p.add_argument("--overlap", action="store_true",
                    help="exchanges on a side stream beside the train passes (TrainerConfig.overlap_comm=True; "
                         "default: serialised on the compute stream, DESIGN.md §7)")
+    p.add_argument("--recompute-h2", action="store_true",
+                   help="A/B: the first train pass of an iteration recomputes layer 2 instead of reading the "
+                        "activations the rollout / critic-values pass stored (TrainerConfig.reuse_h2=False)")
     p.add_argument("--reserve-cus", type=int, default=0,
                    help="CUs kept free of the persistent learner kernels for the side-stream collectives "
                         "(TrainerConfig.reserve_cus)")
@@ -198,6 +201,8 @@ def pg_bench(args, world, rank, dev):
         kw["overlap_comm"] = True
     if args.reserve_cus:
         kw["reserve_cus"] = args.reserve_cus
+    if args.recompute_h2:
+        kw["reuse_h2"] = False
     env, tr = build_pg_workload(args.config, dev, rank=rank, world=world, process_group=pg, envs=args.envs,
                                 horizon=args.horizon, curriculum=args.curriculum, epochs=args.epochs,
                                 minibatches=args.minibatches, **kw)
@@ -486,7 +491,8 @@ def main():
                                None: None}[backend],
                    "ranks_per_gpu": (world + torch.cuda.device_count() - 1) // torch.cuda.device_count()
                    if backend == "gloo" else 1,
-                   "overlap_comm": bool(args.overlap), "reserve_cus": args.reserve_cus},
+                   "overlap_comm": bool(args.overlap), "reserve_cus": args.reserve_cus,
+                   "reuse_h2": not args.recompute_h2},
     }
     out.update(extra)
     # peak torch-allocated device memory of the bench itself (trainer buffers, tapes), read

@@ -81,7 +81,7 @@ class PgRolloutArgs(C.Structure):
                [("diag_flags", C.c_int32), ("success_rule", C.c_int32), ("record_cap", C.c_int32),
                 ("rec_return", C.c_void_p), ("rec_length", C.c_void_p), ("rec_success", C.c_void_p),
                 ("rec_end_step", C.c_void_p), ("ep_code", C.c_void_p), ("applied_act", C.c_void_p),
-                ("dyn_noise_tape", C.c_void_p), ("obs_noise_tape", C.c_void_p)]
+                ("dyn_noise_tape", C.c_void_p), ("obs_noise_tape", C.c_void_p), ("h2_tape", C.c_void_p)]
 
 
 class PgHeadsArgs(C.Structure):
@@ -98,7 +98,7 @@ class PgFusedArgs(C.Structure):
                [(k, C.c_double) for k in ("inv_total_samples", "clip_eps", "vf_coef", "ent_coef")] + \
                [(k, C.c_void_p) for k in ("values", "h1", "dh2", "partial", "loss_partial")] + \
                [("grid", C.c_int32), ("wgrad_splits", C.c_int32), ("wgrad_partial", C.c_void_p),
-                ("grads", C.c_void_p), ("h1_mode", C.c_int32)]
+                ("grads", C.c_void_p), ("h1_mode", C.c_int32), ("h2_in", C.c_void_p), ("h2_out", C.c_void_p)]
 
 
 class SchedArgs(C.Structure):
@@ -177,6 +177,7 @@ _SIGS = {
     "dxrl_pg_fused_pair": (C.c_int, [_I32, C.POINTER(PgFusedArgs), C.POINTER(PgFusedArgs), _P]),
     "dxrl_pg_fused_pair_gnorm": (C.c_int, [_I32, C.POINTER(PgFusedArgs), C.POINTER(PgFusedArgs), _P, _I32,
                                            C.POINTER(_I32), _P]),
+    "dxrl_pg_rollout_kernel": (C.c_int, [C.c_void_p, _I32, C.POINTER(_I32)]),
     "dxrl_pg_gnorm_blocks": (C.c_int, [C.POINTER(_I32)]),
     "dxrl_evaluate": (C.c_int, [_P, C.POINTER(EvalArgs), _P]),
     "dxrl_sched_scratch_bytes": (C.c_int, [_I32, _I32, _I64, _I32, C.POINTER(_I64)]),

@@ -978,6 +978,18 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
 #pragma unroll
             for (int q = 0; q < 4; ++q) MU[(4 * g16 + q) * (kOut + 1) + r16] = acc[q] + b3_reg;
         }
+        if (!aux && mlp && p.h2_tape) {
+            // the step's H2 rows (16 envs x 32 chunks of 16 bytes, chunk c of row r at c ^ r) to
+            // the tape that the actor's train pass reads instead of recomputing layer 2; env lane
+            // et_tid copies chunks et_tid and et_tid + 256 (wave 3 after its head)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int q = et_tid + 256 * u, row = q >> 5, c = q & 31;
+                const int64_t ie = (int64_t)blockIdx.x * kLsEnvs + row;
+                const bf16x8 v = *reinterpret_cast<const bf16x8*>(H2 + row * kHsW + ((c ^ row) << 3));
+                if (ie < n) *reinterpret_cast<bf16x8*>(p.h2_tape + (t * n + ie) * kH2Ld + 8 * c) = v;
+            }
+        }
         if (!kDiag || !(p.diag & 256)) {
             // this step's draws (RW[(t - 1) & 1].rctr: the counters after step t-1's resets)
             if (aux) step_draws(ctr, t);
@@ -1674,6 +1686,33 @@ int dxrl_pg_pack_weights(int32_t device, const float* params, void* packed, void
     return launch_check("k_pack_weights");
 }
 
+}  // extern "C"
+namespace dxrl {
+namespace {
+// The rollout kernel dxrl_pg_rollout launches for n envs: 0 the 64-env reference kernel (feature-
+// major tape / diag 16), 1 the 16-env kernel, 2 the 32-env kernel (>= 32 envs per CU: one round
+// where the 16-env kernel would need two; diag 1024 / 2048 force it / the 16-env kernel).
+int rollout_kernel(int64_t n, int32_t diag_flags, bool obs_fm) {
+    if (obs_fm || (diag_flags & 16)) return 0;
+    static const int cus = [] {
+        int dev = 0, c = 0;
+        (void)hipGetDevice(&dev);
+        return hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0 ? c : 256;
+    }();
+    const bool e8 = !(diag_flags & 2048) && ((diag_flags & 1024) || n >= (int64_t)kE8Envs * cus);
+    return e8 ? 2 : 1;
+}
+}  // namespace
+}  // namespace dxrl
+extern "C" {
+
+int dxrl_pg_rollout_kernel(const dxrl_env* env, int32_t diag_flags, int32_t* kernel) {
+    DXRL_REQUIRE(env && kernel, "null argument");
+    DeviceGuard g(env->device);
+    *kernel = rollout_kernel(env->cfg.num_envs, diag_flags, false);
+    return DXRL_OK;
+}
+
 int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, const dxrl_pg_rollout_args* a,
                     void* stream) {
     DXRL_REQUIRE(env && packed && params && a, "null argument");
@@ -1720,11 +1759,15 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
                     a->ep_code,
                     a->applied_act,
                     a->dyn_noise_tape,
-                    a->obs_noise_tape};
+                    a->obs_noise_tape,
+                    static_cast<bf16*>(a->h2_tape)};
+
     DXRL_REQUIRE(!(a->dyn_noise_tape || a->obs_noise_tape) || !(a->obs_fm || (a->diag_flags & 16)),
                  "the noise tapes are written by the 16- and 32-env rollout kernels only");
     DeviceGuard g(env->device);
     const int64_t n = env->cfg.num_envs;
+    DXRL_REQUIRE(!a->h2_tape || rollout_kernel(n, a->diag_flags, a->obs_fm != nullptr) == 1,
+                 "h2_tape is written by the 16-env rollout kernel only (dxrl_pg_rollout_kernel)");
     if (a->obs_fm || (a->diag_flags & 16)) {  // feature-major tape / A-B reference: the 64-env kernel
         hipLaunchKernelGGL(k_pg_rollout, dim3((unsigned)((n + kTile - 1) / kTile)), dim3(64 * kRolloutWaves), 0,
                            as_stream(stream), p);
@@ -1739,14 +1782,7 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
         stamps_n = n;
     }
     p.stamps = stamps;
-    static const int cus = [] {
-        int dev = 0, c = 0;
-        (void)hipGetDevice(&dev);
-        return hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0 ? c : 256;
-    }();
-    // >= 32 envs per CU: the 32-env kernel runs them in one round (the 16-env kernel would need
-    // two); diag 1024 / 2048 force the 32-env / 16-env kernel (A/B, bit-identity tests)
-    const bool e8 = !(a->diag_flags & 2048) && ((a->diag_flags & 1024) || n >= (int64_t)kE8Envs * cus);
+    const bool e8 = rollout_kernel(n, a->diag_flags, false) == 2;
     if (e8) {
         const bool noise = a->obs_noise_std > 0.0 || a->dyn_noise_std > 0.0 || a->dyn_noise_tape || a->obs_noise_tape;
         const bool diag = (a->diag_flags & ~(1024 | 2048)) != 0 || a->applied_act || a->dyn_noise_tape ||

@@ -96,11 +96,25 @@ struct FusedArgs {
     float* v_out;   // forward mode: [rows]
     bf16* h1_out;   // [rows][kHx] (columns 0..255 written)
     bf16* dh2_out;  // [rows][kH]
+    const bf16* h2_in;  // train, kH2: layer-2 activations [rows][kHp] from the rollout / values pass
+    bf16* h2_out;       // forward (k_pg_values): write H2 [rows][kHp] for the critic's train pass
     float* part;    // [grid][kPartSize]
     double* loss;   // [loss_rows][4]: row b = workgroup b's loss sums, rows >= gridDim.x zeroed
     int loss_rows;  // the caller's row count (dxrl_pg_fused_args.grid)
     unsigned long long* stamps;  // diag & 8: [grid][waves][16] cycles per segment
 };
+
+// one 16-byte-per-lane LDS-DMA piece: lane l's 16 bytes at src land at lds_dst + 16 l (M0 = the
+// wave's LDS destination; global_load_lds_dwordx4, no VGPR staging)
+__device__ __forceinline__ void glds_x4(const void* src, const void* lds_dst) {
+    const uint32_t lds_addr =
+        __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds_dst);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_addr)
+                 : "memory");
+}
 
 __device__ __forceinline__ void zero_acc(f32x16& a) {
 #pragma unroll
@@ -457,8 +471,13 @@ __device__ __forceinline__ bf16x8 wg_frag(const bf16* tile, int col0, int kk, in
 // kNet: 0 actor, 1 critic, -1 read from the arguments; kDiag: the DXRL_FUSED_DIAG ablations /
 // stamps compiled in (production instantiations do not test them at run time: fewer branches and
 // SGPRs in the tile loop)
-template <int kFW, int kTR, bool kTrain, int kNet, bool kDiag>
+// kH2 (train, production geometry): the tile's layer-2 activations come from HBM (p.h2_in,
+// written by the rollout for the actor / by k_pg_values for the critic with the same weights,
+// bit for bit this pass's own L2) by LDS-DMA into the H2 slot while layer 1 runs, instead of
+// being recomputed: no L2 phase (round 6).
+template <int kFW, int kTR, bool kTrain, int kNet, bool kDiag, bool kH2 = false>
 __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedArgs p) {
+    static_assert(!kH2 || (kTrain && kFW == 8 && kTR == 128 && !kDiag), "kH2: production train instantiations");
     const int diag = kDiag ? p.diag : 0;
     const bool actor = kNet < 0 ? p.net == 0 : kNet == 0;  // kNet -1: the net read at run time
     using L = TileLds<kTR>;
@@ -549,12 +568,19 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
     // 160 KB of weight fragments from L2 per tile and workgroup
     constexpr bool kResW = !kTrain && kNT == 1 && DXRL_FWD_RESIDENT_W && DXRL_L2_PIPE;
     constexpr bool kEarlyX = kResW && DXRL_FWD_EARLY_X;
+    // kH2: W1 resident too, so layer 1 issues no global loads -- the LDS-DMA pieces in flight
+    // beside it are invisible to the compiler, and a vmcnt wait for a weight fragment issued
+    // before them would wait for them as well
+    constexpr bool kResW1 = kResW || kH2;
     constexpr bool kDw1Tail = kTrain && kNT == 1 && kMT == 4 && DXRL_DW1_TAIL && DXRL_DH2_IN_DH1;
-    bf16x8 w1res[kResW ? kIn / 16 : 1], w2res[kResW ? kH / 16 : 1];
-    if constexpr (kResW) {
+    bf16x8 w1res[kResW1 ? kIn / 16 : 1], w2res[kResW ? kH / 16 : 1];
+    if constexpr (kResW1) {
         const gbf16x8* p1 = (const gbf16x8*)p.W1 + (int64_t)ft0 * (kIn / 16) * 64 + lane;
 #pragma unroll
         for (int k = 0; k < kIn / 16; ++k) w1res[k] = p1[64 * k];
+    }
+    if constexpr (kH2) __builtin_amdgcn_s_waitcnt(0xF70);  // (vmcnt(0): retired before any LDS-DMA piece)
+    if constexpr (kResW) {
         const gbf16x8* p2 = (const gbf16x8*)p.W2 + (int64_t)ft0 * (kH / 16) * 64 + lane;
 #pragma unroll
         for (int k = 0; k < kH / 16; ++k) w2res[k] = p2[64 * k];
@@ -620,11 +646,36 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         // the first W1 fragments go out before the barrier (their L2 latency overlaps its wait;
         // issued after the X stores, so they do not queue behind the X tile's HBM loads)
         WPre<kIn / 16> pw1;
-        if constexpr (kResW) {
+        if constexpr (kResW1) {
 #pragma unroll
             for (int k = 0; k < kIn / 16; ++k) pw1.wf[k] = w1res[k];
         } else {
             w_prefetch(pw1, W1, kIn / 16, ft0, lane);
+        }
+        // kH2: the head's HBM inputs, then the tile's H2 rows (rows m0 .. m0 + 127 of p.h2_in,
+        // [kTR][kHp] bf16 = 66 contiguous 1 KiB pieces) straight into the H2 slot -- free since the
+        // last tile's end barrier; they land while layer 1 runs
+        float hv2 = 0.0f, adv2 = 0.0f;
+        float4 a02 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (kH2) {
+            const int64_t m16 = m0 + 16 * wave + (lane & 15), mc = m16 < p.rows ? m16 : p.rows - 1;
+            if constexpr (kNet == 1) {
+                hv2 = p.ret[mc];
+            } else {
+                hv2 = p.logp_old[mc];
+                a02 = *reinterpret_cast<const float4*>(p.act + mc * kActPad + 4 * (lane >> 4));
+                adv2 = p.adv[mc];
+            }
+            constexpr int kPieces = kTR * kHp * 2 / 1024;  // 66
+            static_assert(kTR * kHp * 2 % 1024 == 0, "whole 1 KiB pieces");
+            const int64_t valid = (p.rows - m0 < kTR ? p.rows - m0 : kTR) * (int64_t)kHp * 2;  // bytes of real rows
+            const char* src = reinterpret_cast<const char*>(p.h2_in + m0 * kHp);
+            char* dst = reinterpret_cast<char*>(H2);
+            for (int q = wave; q < kPieces; q += kFW) {
+                int64_t off = (int64_t)q * 1024 + 16 * lane;
+                off = off < valid ? off : valid - 16;  // past the last row: a finite copy of real data
+                glds_x4(src + off, dst + q * 1024);
+            }
         }
         STAMP(0);
         __syncthreads();
@@ -642,9 +693,9 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         }
         // the first W2 fragments go out before the barrier (their L2 latency overlaps its wait)
         WPre<kH / 16> pw2;
-        if constexpr (!kResW) w_prefetch(pw2, W2, kH / 16, ft0, lane);
+        if constexpr (!kResW && !kH2) w_prefetch(pw2, W2, kH / 16, ft0, lane);
         STAMP(2);
-        __syncthreads();
+        if constexpr (!kH2) __syncthreads();  // (kH2: no L2, so H1 is next read after the head barrier)
         STAMP(3);
         // head inputs (HBM), issued halfway through L2 so their latency hides behind its second half
         const int ml = 32 * wave + r;
@@ -688,7 +739,7 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             }
         };
 #pragma unroll 1
-        for (int j = 0; j < kNT; ++j) {
+        for (int j = 0; j < (kH2 ? 0 : kNT); ++j) {
             bft = ft0 + j;
             const auto l2_hook = [&]() {
                 if (j == kNT - 1) head_inputs();
@@ -756,6 +807,12 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                     for (int q = 0; q < 8; ++q) b3p[q] = ((gf32*)b3)[(int64_t)((q & 3) + 8 * (q >> 2) + 4 * h) * kHx];
                 }
             }
+        }
+        if constexpr (kH2) {
+            hv = hv2;
+            a0 = a02;
+            adv = adv2;
+            __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): this wave's H2 pieces (and head loads) landed
         }
         STAMP(4);
         __syncthreads();
@@ -990,6 +1047,8 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         }
         STAMP(6);
         if (!kTrain) {
+            // (h2_out: H2 for the critic's train pass, as k_pg_values writes it)
+            if (p.h2_out) copy_tile_out_n<kFThreads, kTR>(H2, p.h2_out, kHp, m0, p.rows, tid, diag);
             if (!kEarlyX && tile + gridDim.x < ntiles) fetch_x(tile + gridDim.x);
             __syncthreads();  // X / H1 / H2 are rewritten by the next tile
             STAMP(7);
@@ -1427,6 +1486,9 @@ __global__ __launch_bounds__(512, 1) void k_pg_values(FusedArgs p) {
             if (k + 2 < ntile) fetch_x(k + 2);
         }
         __syncthreads();  // H2(k) and X(k + 1) complete; H1 free
+        // h2_out: this tile's H2 rows for the critic's train pass (the slot is rewritten only by
+        // the next tile's L2, after the next barrier)
+        if (p.h2_out) copy_tile_out_n<512, 128>(H2, p.h2_out, kHp, row0(k), row0(k) + count(k), tid, 0);
         const auto head = [&]() {  // value head: wave w, samples 16 w .. + 15; V of sample 16 w + l in lane l < 16
             const int s16 = 16 * wave + (lane & 15);
             if (s16 < 32 * mts(k)) {  // (rows past the tile's MFMA tiles were never computed)
@@ -1764,6 +1826,8 @@ int fused_kernel(const dxrl_pg_fused_args* a, hipStream_t st, int* grid_out) {
     const bool recompute = train && a->rows % 32 == 0 && a->h1_mode == 0;
     f.h1_out = recompute ? nullptr : static_cast<bf16*>(a->h1);
     f.dh2_out = static_cast<bf16*>(a->dh2);
+    f.h2_in = train ? static_cast<const bf16*>(a->h2_in) : nullptr;
+    f.h2_out = train ? nullptr : static_cast<bf16*>(a->h2_out);
     f.part = a->partial;
     f.loss = a->loss_partial;
     f.loss_rows = a->grid;
@@ -1806,10 +1870,14 @@ int fused_kernel(const dxrl_pg_fused_args* a, hipStream_t st, int* grid_out) {
         else if (DXRL_FWD_VALUES && !layered) hipLaunchKernelGGL(k_pg_values, dim3(grid), dim3(512), 0, st, f);
         else hipLaunchKernelGGL((k_pg_fused<8, 128, false, 1, false>), dim3(grid), dim3(512), 0, st, f);
     } else if (!c) {
+        // (h2_in: the layer-2 activations from the rollout; the diagnostic instantiations recompute
+        // them -- the same bits either way)
         if (dg) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 0, true>), dim3(grid), dim3(512), 0, st, f);
+        else if (f.h2_in) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 0, false, true>), dim3(grid), dim3(512), 0, st, f);
         else hipLaunchKernelGGL((k_pg_fused<8, 128, true, 0, false>), dim3(grid), dim3(512), 0, st, f);
     } else {
         if (dg) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 1, true>), dim3(grid), dim3(512), 0, st, f);
+        else if (f.h2_in) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 1, false, true>), dim3(grid), dim3(512), 0, st, f);
         else hipLaunchKernelGGL((k_pg_fused<8, 128, true, 1, false>), dim3(grid), dim3(512), 0, st, f);
     }
     if (int rc = launch_check("k_pg_fused")) return rc;

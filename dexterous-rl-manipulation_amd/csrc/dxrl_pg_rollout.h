@@ -42,9 +42,11 @@ struct PgRolloutArgs {
     float* applied_act;  // [T N][kActPad] the action the env integrated (nullable; parity checks)
     float* dyn_noise_tape;  // [T N][kActPad] f32(sigma) * z as added to the action (nullable; ws kernel)
     float* obs_noise_tape;  // [(T+1) N][kObsNoiseLd] f32(sigma) * z per observation element (nullable)
+    bf16* h2_tape;          // [T N][kH2Ld] the actor's layer-2 activations of every step (nullable)
     unsigned long long* stamps;  // diag & 128: cycles per step segment (16- / 32-env kernels)
 };
 constexpr int kObsNoiseLd = 48;
+constexpr int kH2Ld = 264;  // h2_tape row pitch (bf16): the fused learner's H2 tile rows (kHp)
 
 // Workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding
 // global store (s_waitcnt vmcnt(0)) before s_barrier, which puts the tape stores' write

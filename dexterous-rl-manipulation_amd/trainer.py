@@ -37,6 +37,7 @@ from .envs import VecEnv
 
 # csrc/dxrl_pg.h
 OBS_IN, IN, H, HX, OUT, ACT, ACT_PAD = 45, 64, 256, 288, 32, 15, 16
+H2LD = 264  # row pitch (bf16) of the stored layer-2 activations: the fused learner's H2 tile rows
 W1, W2, W3 = H * IN, H * HX, OUT * HX
 OFF = {"W1a": 0, "W2a": W1, "W3a": W1 + W2, "logstd": W1 + W2 + W3}
 OFF["W1c"] = OFF["logstd"] + 32
@@ -110,6 +111,12 @@ class TrainerConfig:
     # (dxrl_pg_adam_step) instead of a k_sumsq pass over the gradient -- one launch fewer per
     # update; the norm's f64 sum order differs (agrees to f64 rounding)
     fused_gnorm: bool = True
+    # the layer-2 activations of each network computed once per weight version (round 6): the
+    # rollout writes the actor's H2 of every sample (16-env rollout kernel), the critic-values pass
+    # writes the critic's, and the first train pass under those weights reads them instead of
+    # recomputing layer 2 (bit-identical: same MFMA k order and tanh); later PPO passes, after an
+    # optimiser step, recompute.  Memory: two [M][264] bf16 buffers (0.43 GB each at C2)
+    reuse_h2: bool = True
 
 
 def minibatch_bounds(M: int, B: int, round_samples: int):
@@ -274,6 +281,12 @@ class PGTrainer:
             nbk = C.c_int32()
             N.call("dxrl_pg_gnorm_blocks", C.byref(nbk))
             self.gn_partial = torch.zeros(nbk.value, dtype=torch.float64, device=d)
+        # layer-2 activations for the first train pass of a weight version (cfg.reuse_h2)
+        self.h2a = self.h2c = None
+        self._h2a_fresh = self._h2c_fresh = False
+        if cfg.fused and cfg.reuse_h2:
+            self.h2a = z(M, H2LD, dt=bf)  # zero padding columns (the learner's LDS-DMA reads them)
+            self.h2c = z(M + n, H2LD, dt=bf)
         self.pack()
 
     @property
@@ -310,6 +323,7 @@ class PGTrainer:
 
     def pack(self):
         N.call("dxrl_pg_pack_weights", self.dev.index, N.ptr(self.params), N.ptr(self.packed), self._s())
+        self._h2a_fresh = self._h2c_fresh = False  # new weights: the stored activations are stale
 
     def _s(self):
         return N.stream_of(self.dev)
@@ -350,7 +364,15 @@ class PGTrainer:
         a.applied_act = p(getattr(self, "applied_act", None))  # parity tapes (tests only; None in runs)
         a.dyn_noise_tape = p(getattr(self, "dyn_noise_tape", None))
         a.obs_noise_tape = p(getattr(self, "obs_noise_tape", None))
+        # the actor's H2 tape (the 16-env kernel writes it; the 32-env one has no registers left)
+        tape = False
+        if self.h2a is not None:
+            k = C.c_int32()
+            N.call("dxrl_pg_rollout_kernel", self.env.handle, self.diag_flags, C.byref(k))
+            tape = k.value == 1
+        a.h2_tape = p(self.h2a) if tape else None
         N.call("dxrl_pg_rollout", self.env.handle, p(self.packed), p(self.params), C.byref(a), self._s())
+        self._h2a_fresh = tape
 
     def _mlp_forward(self, net, rows, H1, H2, head_f32=None, head_fm=None, ld_head_fm=0):
         P = self.params
@@ -385,6 +407,8 @@ class PGTrainer:
         f.partial, f.loss_partial, f.grid = p(self.fused_partial), p(self.fused_loss), self.fused_grid
         f.wgrad_splits, f.wgrad_partial, f.grads = self.splits, p(self.kpartial), p(self.grads)
         f.h1_mode = 0 if c.h1_recompute else 1
+        if train and (self._h2c_fresh if net == 1 else self._h2a_fresh):
+            f.h2_in = p((self.h2c if net == 1 else self.h2a)[start:])
         return f
 
     def train(self):
@@ -410,7 +434,10 @@ class PGTrainer:
 
     def critic_values(self):
         """V over the T + 1 observation blocks (fused forward, nothing stored but V)."""
-        N.call("dxrl_pg_fused", self.dev.index, C.byref(self._fused_args(1, False, self.M + self.n)), self._s())
+        f = self._fused_args(1, False, self.M + self.n)
+        f.h2_out = N.ptr(self.h2c)
+        N.call("dxrl_pg_fused", self.dev.index, C.byref(f), self._s())
+        self._h2c_fresh = self.h2c is not None
 
     def actor_train(self):
         start, rows = self._mb
@@ -556,6 +583,7 @@ class PGTrainer:
                    N.ptr(self.packed), self._s())
         self._spare = (self.params, self.m1, self.m2)
         self.params, self.m1, self.m2 = po, m1o, m2o
+        self._h2a_fresh = self._h2c_fresh = False  # new weights: the stored activations are stale
 
     def attach_curriculum(self, scheduler):
         """Host-side CurriculumScheduler (experiments/curriculum_scheduler.py) fed with every

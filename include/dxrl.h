@@ -296,12 +296,19 @@ typedef struct dxrl_pg_rollout_args {
        adds f32(n) to the action; :199-207 adds f32(n) to every observation element. */
     float* dyn_noise_tape;     /* f32 [T N][16] dynamics noise per action dim (0 if off)    */
     float* obs_noise_tape;     /* f32 [(T+1) N][48] observation noise per obs element       */
+    void* h2_tape;             /* bf16 [T N][264] the actor's layer-2 activations of every step
+                                  (nullable; the 16- and 32-env kernels; dxrl_pg_fused_args.h2_in of
+                                  the actor's first train pass under these weights)            */
 } dxrl_pg_rollout_args;
 
 /* Fused policy + env rollout: T steps of actor MLP (bf16 MFMA) -> Gaussian
  * sample -> [dynamics noise] -> env step -> tape, auto-reset (device RNG). */
 int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, const dxrl_pg_rollout_args* args,
                     void* stream);
+/* Which kernel dxrl_pg_rollout runs for this env and diag_flags (without a feature-major tape):
+ * 1 the 16-env kernel (< 32 envs per CU; the only one that writes h2_tape), 2 the 32-env kernel,
+ * 0 the 64-env reference kernel (diag_flags & 16).  Host-only query. */
+int dxrl_pg_rollout_kernel(const dxrl_env* env, int32_t diag_flags, int32_t* kernel);
 
 /* GAE reverse scan; values f32 [(T+1) N]; writes adv/ret [T N] and this rank's advantage
  * moments stats[5] = T N, stats[6] = mean(adv), stats[7] = sum of squared deviations, and
@@ -489,6 +496,14 @@ typedef struct dxrl_pg_fused_args {
     float* wgrad_partial;      /* f32 [wgrad_splits + 16][256][288]                        */
     float* grads;              /* f32 master-layout gradients: W1/W2/W3 (+ log_std) blocks */
     int32_t h1_mode;           /* 0 recompute H1 for dW2 when rows % 32 == 0, 1 HBM copy    */
+    /* Layer-2 activations computed once per weight version (round 6; both nullable):
+       h2_out (forward mode): bf16 [rows][264] H2 of the critic, written by the values pass;
+       h2_in (train mode): bf16 [rows][264] H2 of this net under the SAME weights -- the rollout's
+       h2_tape for the actor, the values pass's h2_out for the critic -- read instead of
+       recomputing layer 2 (bit-identical: same MFMA k order and tanh).  Columns 256..263 are
+       padding (keep them finite, e.g. zero-initialised). */
+    const void* h2_in;
+    void* h2_out;
 } dxrl_pg_fused_args;
 
 int dxrl_pg_fused_sizes(int32_t* tile_rows, int64_t* partial_floats_per_block);

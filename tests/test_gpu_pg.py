@@ -216,6 +216,59 @@ def test_paired_learner_equals_two_passes(pkg, n, T, mb):
         assert torch.equal(la, lb)
 
 
+@pytest.mark.parametrize("n,T,mb,paired", [(4096, 32, 1, True), (773, 32, 1, True), (2048, 32, 4, True),
+                                          (1001, 32, 1, False), (8192, 8, 1, True), (5, 32, 1, True)])
+def test_stored_h2_equals_recomputed(pkg, n, T, mb, paired):
+    """TrainerConfig.reuse_h2: the actor's layer-2 activations written by the rollout (16-env
+    kernel) and the critic's written by the critic-values pass, read by the first train passes
+    under those weights (LDS-DMA into the H2 tile), give the recomputing passes' results bit for
+    bit: V, every minibatch's gradients, loss sums and dH2 of both networks.  Ragged tiles, PPO
+    slices, the per-network path, 8192 envs (32-env rollout kernel: no actor tape, the critic's
+    still read), and fewer rows than one tile."""
+    outs = []
+    for reuse in (True, False):
+        _, tr = make(pkg, n, T, minibatches=mb, reuse_h2=reuse)
+        if not paired:
+            tr.paired = False
+        tr.rollout()
+        tr.critic_values()
+        tr.advantages()
+        torch.cuda.synchronize()
+        if reuse:  # what the passes below read
+            assert tr._h2c_fresh and tr._h2a_fresh == (n < 32 * torch.cuda.get_device_properties(0).multi_processor_count)
+        b = tr.minibatch_bounds()
+        got = [tr.V.clone()]
+        for k in range(mb):
+            tr._mb = (b[k], b[k + 1] - b[k])
+            tr.train_passes()
+            torch.cuda.synchronize()
+            rows = b[k + 1] - b[k]
+            got.append((tr.grads.clone(), tr.fused_loss.clone(), tr.dH2[:rows].clone(),
+                        tr.dH2c[:rows].clone() if tr.dH2c is not None and paired else None))
+        outs.append(got)
+    va, vb = outs[0][0], outs[1][0]
+    assert torch.equal(va, vb)
+    for x, y in zip(outs[0][1:], outs[1][1:]):
+        for u, w in zip(x, y):
+            if u is not None:
+                assert torch.equal(u, w)
+
+
+def test_stored_h2_is_refreshed_after_every_update(pkg):
+    """PPO 2 x 2 through iteration(): only the first train pair of an iteration reads the stored
+    activations (the optimiser step makes them stale); parameters after two iterations equal the
+    recomputing trainer's bit for bit."""
+    params = []
+    for reuse in (True, False):
+        _, tr = make(pkg, 1024, 32, epochs=2, minibatches=2, reuse_h2=reuse)
+        for _ in range(2):
+            tr.iteration()
+            assert not tr._h2a_fresh and not tr._h2c_fresh
+        torch.cuda.synchronize()
+        params.append(tr.params.clone())
+    assert torch.equal(params[0], params[1])
+
+
 @pytest.mark.parametrize("n,T,mb,max_norm", [(256, 32, 1, 0.5), (2048, 32, 4, 1e-3), (512, 32, 1, 1e6)])
 def test_reduction_gnorm_partials_match_sumsq_path(pkg, n, T, mb, max_norm):
     """One rank, paired step (TrainerConfig.fused_gnorm): the grad-norm partials written by the

@@ -1488,7 +1488,19 @@ __global__ __launch_bounds__(512, 1) void k_pg_values(FusedArgs p) {
         __syncthreads();  // H2(k) and X(k + 1) complete; H1 free
         // h2_out: this tile's H2 rows for the critic's train pass (the slot is rewritten only by
         // the next tile's L2, after the next barrier)
-        if (p.h2_out) copy_tile_out_n<512, 128>(H2, p.h2_out, kHp, row0(k), row0(k) + count(k), tid, 0);
+        if (p.h2_out) {
+            // non-temporal stores: the stream is read back once, by the critic's train pass (plain
+            // stores: iteration 1.66-1.67 vs 1.62-1.63 ms, profiles/r06/ab_h2_variants.log; the
+            // copy spread over the next layer 1's steps was slower still, ab_h2_spread_rejected.log)
+            const int64_t h2_m0 = row0(k), h2_end = row0(k) + count(k);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int c = tid + 512 * u, row = c >> 5, col = 8 * (c & 31);
+                const bf16x8 v = *reinterpret_cast<const bf16x8*>(H2 + row * kHp + col);
+                if (h2_m0 + row < h2_end)
+                    __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p.h2_out + (h2_m0 + row) * kHp + col));
+            }
+        }
         const auto head = [&]() {  // value head: wave w, samples 16 w .. + 15; V of sample 16 w + l in lane l < 16
             const int s16 = 16 * wave + (lane & 15);
             if (s16 < 32 * mts(k)) {  // (rows past the tile's MFMA tiles were never computed)

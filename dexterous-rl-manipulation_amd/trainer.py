@@ -115,7 +115,9 @@ class TrainerConfig:
     # rollout writes the actor's H2 of every sample (16-env rollout kernel), the critic-values pass
     # writes the critic's, and the first train pass under those weights reads them instead of
     # recomputing layer 2 (bit-identical: same MFMA k order and tanh); later PPO passes, after an
-    # optimiser step, recompute.  Memory: two [M][264] bf16 buffers (0.43 GB each at C2)
+    # optimiser step, recompute.  Memory: [M][264] bf16 for the actor (0.43 GB at C2), and as
+    # much for the critic when epochs x minibatches == 1 (else its store would cost more than the
+    # first minibatch pass saves)
     reuse_h2: bool = True
 
 
@@ -286,7 +288,10 @@ class PGTrainer:
         self._h2a_fresh = self._h2c_fresh = False
         if cfg.fused and cfg.reuse_h2:
             self.h2a = z(M, H2LD, dt=bf)  # zero padding columns (the learner's LDS-DMA reads them)
-            self.h2c = z(M + n, H2LD, dt=bf)
+            # the critic's only when one full-batch train pass reads it: the values pass pays the
+            # store (≈40 µs at C2) on every iteration, a PPO minibatch pass saves a quarter of it
+            if cfg.epochs * cfg.minibatches == 1:
+                self.h2c = z(M + n, H2LD, dt=bf)
         self.pack()
 
     @property
@@ -435,7 +440,7 @@ class PGTrainer:
     def critic_values(self):
         """V over the T + 1 observation blocks (fused forward, nothing stored but V)."""
         f = self._fused_args(1, False, self.M + self.n)
-        f.h2_out = N.ptr(self.h2c)
+        f.h2_out = N.ptr(self.h2c)  # (None: not stored)
         N.call("dxrl_pg_fused", self.dev.index, C.byref(f), self._s())
         self._h2c_fresh = self.h2c is not None
 

@@ -987,7 +987,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_pg_rollout_ws(PgRolloutArgs p
                 const int q = et_tid + 256 * u, row = q >> 5, c = q & 31;
                 const int64_t ie = (int64_t)blockIdx.x * kLsEnvs + row;
                 const bf16x8 v = *reinterpret_cast<const bf16x8*>(H2 + row * kHsW + ((c ^ row) << 3));
-                if (ie < n) *reinterpret_cast<bf16x8*>(p.h2_tape + (t * n + ie) * kH2Ld + 8 * c) = v;
+                if (ie < n)  // non-temporal: read back once, by the actor's train pass (ab_h2_tape_nt.log)
+                    __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p.h2_tape + (t * n + ie) * kH2Ld + 8 * c));
             }
         }
         if (!kDiag || !(p.diag & 256)) {

@@ -259,11 +259,17 @@ def pg_bench(args, world, rank, dev):
     gemm_ms = sum(v for k, v in phases.items() if k not in ("rollout", "advantages", "optimizer_step",
                                                             "schedule_feed", "schedule_apply"))
     train_flops = M * args.epochs * (FWD_BOTH + BWD_BOTH)
+    # (reuse_h2: the first train pass reads the actor's layer 2 from the rollout's tape -- computed in
+    # the rollout phase, outside gemm_ms -- so that pass's share of it is not counted here; the
+    # critic's comes from the critic-values pass, inside gemm_ms)
+    l2_from_rollout = M * 2 * 256 * 256 if getattr(tr, "h2a_tape_written", False) else 0
+    train_flops -= l2_from_rollout
     mfma = {"bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_BF16_TFS,
             "training_gemms_achieved": round(train_flops / (gemm_ms * 1e-3) / 1e12, 2),
             "rollout_policy_achieved": round(M * FWD_ACTOR / (phases["rollout"] * 1e-3) / 1e12, 2),
             "algorithmic_flop_per_env_step": {"rollout_actor_fwd": FWD_ACTOR, "train_fwd": FWD_BOTH,
-                                              "train_bwd": BWD_BOTH}}
+                                              "train_bwd": BWD_BOTH},
+            "train_l2_read_from_rollout_flop": l2_from_rollout}
     mfma["frac"] = round(mfma["training_gemms_achieved"] / PEAK_BF16_TFS, 4)
     stats = tr.episode_stats()
     if tr.scheduler is not None:

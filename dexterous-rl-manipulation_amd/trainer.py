@@ -285,7 +285,7 @@ class PGTrainer:
             self.gn_partial = torch.zeros(nbk.value, dtype=torch.float64, device=d)
         # layer-2 activations for the first train pass of a weight version (cfg.reuse_h2)
         self.h2a = self.h2c = None
-        self._h2a_fresh = self._h2c_fresh = False
+        self._h2a_fresh = self._h2c_fresh = self.h2a_tape_written = False
         if cfg.fused and cfg.reuse_h2:
             self.h2a = z(M, H2LD, dt=bf)  # zero padding columns (the learner's LDS-DMA reads them)
             # the critic's only when one full-batch train pass reads it: the values pass pays the
@@ -377,7 +377,7 @@ class PGTrainer:
             tape = k.value == 1
         a.h2_tape = p(self.h2a) if tape else None
         N.call("dxrl_pg_rollout", self.env.handle, p(self.packed), p(self.params), C.byref(a), self._s())
-        self._h2a_fresh = tape
+        self._h2a_fresh = self.h2a_tape_written = tape
 
     def _mlp_forward(self, net, rows, H1, H2, head_f32=None, head_fm=None, ld_head_fm=0):
         P = self.params

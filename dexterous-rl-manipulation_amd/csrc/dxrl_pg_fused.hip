@@ -454,6 +454,16 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #define DXRL_DW1_TAIL 1
 #endif
 
+// kH2: workgroup group g = (blockIdx / 8) % DXRL_H2_SKEW_GROUPS starts its tile loop g x
+// DXRL_H2_SKEW x 4096 cycles late, so that the groups' per-tile 66 KiB H2 bursts do not all hit HBM
+// in the same layer-1 window (0: no skew)
+#ifndef DXRL_H2_SKEW
+#define DXRL_H2_SKEW 0
+#endif
+#ifndef DXRL_H2_SKEW_GROUPS
+#define DXRL_H2_SKEW_GROUPS 2
+#endif
+
 // dW3 / dW1 operands through tr_frag16_eo (even / odd sample order inside each 8-sample group:
 // the transposed reads conflict-free) instead of tr_frag16 (2-way)
 #ifndef DXRL_TR_EO
@@ -616,6 +626,10 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 w3res[k] = (lane & 15) == 0 ? *(const gbf16x8*)(p.W3rm + 32 * k + 8 * (lane >> 4)) : zero8();
             b3res = ((gf32*)p.b3)[0];
         }
+    }
+    if constexpr (kH2 && DXRL_H2_SKEW > 0) {
+        const int g = (int)(blockIdx.x >> 3) % DXRL_H2_SKEW_GROUPS;
+        for (int i = 0; i < g * DXRL_H2_SKEW; ++i) __builtin_amdgcn_s_sleep(64);
     }
     int64_t tile = blockIdx.x;
     if (tile < ntiles) fetch_x(tile);

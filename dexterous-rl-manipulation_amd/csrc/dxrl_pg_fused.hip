@@ -454,14 +454,9 @@ __device__ __forceinline__ T* opaque(T* ptr) {
 #define DXRL_DW1_TAIL 1
 #endif
 
-// kH2: workgroup group g = (blockIdx / 8) % DXRL_H2_SKEW_GROUPS starts its tile loop g x
-// DXRL_H2_SKEW x 4096 cycles late, so that the groups' per-tile 66 KiB H2 bursts do not all hit HBM
-// in the same layer-1 window (0: no skew)
-#ifndef DXRL_H2_SKEW
-#define DXRL_H2_SKEW 0
-#endif
-#ifndef DXRL_H2_SKEW_GROUPS
-#define DXRL_H2_SKEW_GROUPS 2
+// stamps (DXRL_FUSED_DIAG=8) of the kH2 passes: a diagnostic build only
+#ifndef DXRL_H2_STAMPS
+#define DXRL_H2_STAMPS 0
 #endif
 
 // dW3 / dW1 operands through tr_frag16_eo (even / odd sample order inside each 8-sample group:
@@ -487,7 +482,7 @@ __device__ __forceinline__ bf16x8 wg_frag(const bf16* tile, int col0, int kk, in
 // being recomputed: no L2 phase (round 6).
 template <int kFW, int kTR, bool kTrain, int kNet, bool kDiag, bool kH2 = false>
 __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedArgs p) {
-    static_assert(!kH2 || (kTrain && kFW == 8 && kTR == 128 && !kDiag), "kH2: production train instantiations");
+    static_assert(!kH2 || (kTrain && kFW == 8 && kTR == 128 && (!kDiag || DXRL_H2_STAMPS)), "kH2: production train instantiations");
     const int diag = kDiag ? p.diag : 0;
     const bool actor = kNet < 0 ? p.net == 0 : kNet == 0;  // kNet -1: the net read at run time
     using L = TileLds<kTR>;
@@ -626,10 +621,6 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 w3res[k] = (lane & 15) == 0 ? *(const gbf16x8*)(p.W3rm + 32 * k + 8 * (lane >> 4)) : zero8();
             b3res = ((gf32*)p.b3)[0];
         }
-    }
-    if constexpr (kH2 && DXRL_H2_SKEW > 0) {
-        const int g = (int)(blockIdx.x >> 3) % DXRL_H2_SKEW_GROUPS;
-        for (int i = 0; i < g * DXRL_H2_SKEW; ++i) __builtin_amdgcn_s_sleep(64);
     }
     int64_t tile = blockIdx.x;
     if (tile < ntiles) fetch_x(tile);
@@ -1898,11 +1889,13 @@ int fused_kernel(const dxrl_pg_fused_args* a, hipStream_t st, int* grid_out) {
     } else if (!c) {
         // (h2_in: the layer-2 activations from the rollout; the diagnostic instantiations recompute
         // them -- the same bits either way)
-        if (dg) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 0, true>), dim3(grid), dim3(512), 0, st, f);
+        if (dg && DXRL_H2_STAMPS && f.h2_in) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 0, true, DXRL_H2_STAMPS != 0>), dim3(grid), dim3(512), 0, st, f);
+        else if (dg) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 0, true>), dim3(grid), dim3(512), 0, st, f);
         else if (f.h2_in) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 0, false, true>), dim3(grid), dim3(512), 0, st, f);
         else hipLaunchKernelGGL((k_pg_fused<8, 128, true, 0, false>), dim3(grid), dim3(512), 0, st, f);
     } else {
-        if (dg) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 1, true>), dim3(grid), dim3(512), 0, st, f);
+        if (dg && DXRL_H2_STAMPS && f.h2_in) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 1, true, DXRL_H2_STAMPS != 0>), dim3(grid), dim3(512), 0, st, f);
+        else if (dg) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 1, true>), dim3(grid), dim3(512), 0, st, f);
         else if (f.h2_in) hipLaunchKernelGGL((k_pg_fused<8, 128, true, 1, false, true>), dim3(grid), dim3(512), 0, st, f);
         else hipLaunchKernelGGL((k_pg_fused<8, 128, true, 1, false>), dim3(grid), dim3(512), 0, st, f);
     }

@@ -657,11 +657,17 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
         } else {
             w_prefetch(pw1, W1, kIn / 16, ft0, lane);
         }
-        // kH2: the head's HBM inputs, then the tile's H2 rows (rows m0 .. m0 + 127 of p.h2_in,
-        // [kTR][kHp] bf16 = 66 contiguous 1 KiB pieces) straight into the H2 slot -- free since the
-        // last tile's end barrier; they land while layer 1 runs
+        // kH2: the head's HBM inputs here; the tile's H2 rows (rows m0 .. m0 + 127 of p.h2_in, [kTR][kHp]
+        // bf16 = 66 contiguous 1 KiB pieces) go straight into the H2 slot -- free since the last tile's
+        // end barrier -- at layer 1's first k-step, issued by waves 4..7 only (16-17 pieces each).
+        // Issuing stalls a wave for ~2.4 k cycles per tile (the CU's memory path); waves 4..7 are the
+        // s_setprio 1 half, so while one stalls its SIMD runs the partner's layer 1 (issued by every
+        // wave before the barrier instead, the stall sat on every wave's path: profiles/r06/
+        // ab_h2_dma_waves47_sched.log, fused_stamps_h2_dma_place.log)
         float hv2 = 0.0f, adv2 = 0.0f;
         float4 a02 = make_float4(0.f, 0.f, 0.f, 0.f);
+        constexpr int kPieces = kTR * kHp * 2 / 1024;  // 66
+        static_assert(kTR * kHp * 2 % 1024 == 0, "whole 1 KiB pieces");
         if constexpr (kH2) {
             const int64_t m16 = m0 + 16 * wave + (lane & 15), mc = m16 < p.rows ? m16 : p.rows - 1;
             if constexpr (kNet == 1) {
@@ -671,17 +677,21 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
                 a02 = *reinterpret_cast<const float4*>(p.act + mc * kActPad + 4 * (lane >> 4));
                 adv2 = p.adv[mc];
             }
-            constexpr int kPieces = kTR * kHp * 2 / 1024;  // 66
-            static_assert(kTR * kHp * 2 % 1024 == 0, "whole 1 KiB pieces");
-            const int64_t valid = (p.rows - m0 < kTR ? p.rows - m0 : kTR) * (int64_t)kHp * 2;  // bytes of real rows
-            const char* src = reinterpret_cast<const char*>(p.h2_in + m0 * kHp);
-            char* dst = reinterpret_cast<char*>(H2);
-            for (int q = wave; q < kPieces; q += kFW) {
-                int64_t off = (int64_t)q * 1024 + 16 * lane;
-                off = off < valid ? off : valid - 16;  // past the last row: a finite copy of real data
-                glds_x4(src + off, dst + q * 1024);
-            }
         }
+        const bool h2_issuer = kH2 && __builtin_amdgcn_readfirstlane(wave) >= kFW / 2;
+        const auto h2_dma_k = [&](int sidx) {
+            if constexpr (kH2) {
+                if (sidx != 0 || !h2_issuer) return;
+                const int64_t valid = (p.rows - m0 < kTR ? p.rows - m0 : kTR) * (int64_t)kHp * 2;  // bytes of real rows
+                const char* src = reinterpret_cast<const char*>(p.h2_in + m0 * kHp);
+                char* dst = reinterpret_cast<char*>(H2);
+                for (int q = __builtin_amdgcn_readfirstlane(wave) - kFW / 2; q < kPieces; q += kFW / 2) {
+                    int64_t off = (int64_t)q * 1024 + 16 * lane;
+                    off = off < valid ? off : valid - 16;  // past the last row: a finite copy of real data
+                    glds_x4(src + off, dst + q * 1024);
+                }
+            }
+        };
         STAMP(0);
         __syncthreads();
         STAMP(1);
@@ -694,7 +704,8 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             // bias = W1 column 45 (X column 45 = 1)
             if (j > 0) w_prefetch(pw1, W1, kIn / 16, ft0 + j, lane);
             EpiTanh e1{H1, 32 * (ft0 + j) + 4 * h, r, nullptr};
-            fwd_pipe<kIn / 16, kXp, kMT>(pw1, X, lane, e1);
+            if constexpr (kH2) fwd_pipe<kIn / 16, kXp, kMT>(pw1, X, lane, e1, NoHook{}, false, h2_dma_k);
+            else fwd_pipe<kIn / 16, kXp, kMT>(pw1, X, lane, e1);
         }
         // the first W2 fragments go out before the barrier (their L2 latency overlaps its wait)
         WPre<kH / 16> pw2;
@@ -817,7 +828,10 @@ __global__ __launch_bounds__(64 * kFW, kTR == 64 ? 2 : 1) void k_pg_fused(FusedA
             hv = hv2;
             a0 = a02;
             adv = adv2;
-            __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): this wave's H2 pieces (and head loads) landed
+            // vmcnt(0) on the issuing waves: their H2 pieces landed before the head barrier (the other
+            // waves' own loads are waited for by the compiler where they are used; a vmcnt(0) there
+            // too only waited out the head's weight loads: profiles/r06/ab_h2_dma_wait_issuers.log)
+            if (h2_issuer) __builtin_amdgcn_s_waitcnt(0xF70);
         }
         STAMP(4);
         __syncthreads();

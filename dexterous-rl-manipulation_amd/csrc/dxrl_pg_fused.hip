@@ -1510,7 +1510,8 @@ __global__ __launch_bounds__(512, 1) void k_pg_values(FusedArgs p) {
         if (p.h2_out) {
             // non-temporal stores: the stream is read back once, by the critic's train pass (plain
             // stores: iteration 1.66-1.67 vs 1.62-1.63 ms, profiles/r06/ab_h2_variants.log; the
-            // copy spread over the next layer 1's steps was slower still, ab_h2_spread_rejected.log)
+            // copy spread over the next layer 1's steps was slower still, ab_h2_spread_rejected.log;
+            // issued by waves 4..7 only: no change, ab_values_h2_half_rejected.log)
             const int64_t h2_m0 = row0(k), h2_end = row0(k) + count(k);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {

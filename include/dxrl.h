@@ -297,8 +297,9 @@ typedef struct dxrl_pg_rollout_args {
     float* dyn_noise_tape;     /* f32 [T N][16] dynamics noise per action dim (0 if off)    */
     float* obs_noise_tape;     /* f32 [(T+1) N][48] observation noise per obs element       */
     void* h2_tape;             /* bf16 [T N][264] the actor's layer-2 activations of every step
-                                  (nullable; the 16- and 32-env kernels; dxrl_pg_fused_args.h2_in of
-                                  the actor's first train pass under these weights)            */
+                                  (nullable; written by the 16-env kernel only, see
+                                  dxrl_pg_rollout_kernel; dxrl_pg_fused_args.h2_in of the actor's
+                                  first train pass under these weights)                        */
 } dxrl_pg_rollout_args;
 
 /* Fused policy + env rollout: T steps of actor MLP (bf16 MFMA) -> Gaussian

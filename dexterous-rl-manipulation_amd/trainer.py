@@ -287,7 +287,8 @@ class PGTrainer:
         self.h2a = self.h2c = None
         self._h2a_fresh = self._h2c_fresh = self.h2a_tape_written = False
         if cfg.fused and cfg.reuse_h2:
-            self.h2a = z(M, H2LD, dt=bf)  # zero padding columns (the learner's LDS-DMA reads them)
+            # the actor's tape is allocated by the first rollout that runs the 16-env kernel (the
+            # only one that writes it: not at C4's 8192 envs, where it would be 0.86 GB unused)
             # the critic's only when one full-batch train pass reads it: the values pass pays the
             # store (≈40 µs at C2) on every iteration, a PPO minibatch pass saves a quarter of it
             if cfg.epochs * cfg.minibatches == 1:
@@ -371,10 +372,12 @@ class PGTrainer:
         a.obs_noise_tape = p(getattr(self, "obs_noise_tape", None))
         # the actor's H2 tape (the 16-env kernel writes it; the 32-env one has no registers left)
         tape = False
-        if self.h2a is not None:
+        if self.cfg.fused and self.cfg.reuse_h2:
             k = C.c_int32()
             N.call("dxrl_pg_rollout_kernel", self.env.handle, self.diag_flags, C.byref(k))
             tape = k.value == 1
+            if tape and self.h2a is None:  # zero padding columns (the learner's LDS-DMA reads them)
+                self.h2a = torch.zeros(self.M, H2LD, dtype=torch.bfloat16, device=self.dev)
         a.h2_tape = p(self.h2a) if tape else None
         N.call("dxrl_pg_rollout", self.env.handle, p(self.packed), p(self.params), C.byref(a), self._s())
         self._h2a_fresh = self.h2a_tape_written = tape

@@ -1692,6 +1692,9 @@ int dxrl_pg_fused(int32_t device, const dxrl_pg_fused_args* a, void* stream) {
         DXRL_REQUIRE((reinterpret_cast<uintptr_t>(a->act) & 15) == 0, "fused: act must be 16-byte aligned");
     }
     DXRL_REQUIRE((reinterpret_cast<uintptr_t>(a->obs) & 15) == 0, "fused: obs must be 16-byte aligned");
+    // (read by 16-byte LDS-DMA pieces / written by 16-byte stores)
+    DXRL_REQUIRE(((reinterpret_cast<uintptr_t>(a->h2_in) | reinterpret_cast<uintptr_t>(a->h2_out)) & 15) == 0,
+                 "fused: h2_in / h2_out must be 16-byte aligned");
     DeviceGuard g(device);
     hipStream_t st = as_stream(stream);
     int grid = 0;
@@ -1785,6 +1788,7 @@ int dxrl_pg_fused_pair_gnorm(int32_t device, const dxrl_pg_fused_args* c, const 
         DXRL_REQUIRE(((reinterpret_cast<uintptr_t>(x->partial) | reinterpret_cast<uintptr_t>(x->wgrad_partial) |
                        reinterpret_cast<uintptr_t>(x->obs) | reinterpret_cast<uintptr_t>(x->act)) & 15) == 0,
                      "fused_pair: partial / wgrad_partial / obs / act must be 16-byte aligned");
+        DXRL_REQUIRE((reinterpret_cast<uintptr_t>(x->h2_in) & 15) == 0, "fused_pair: h2_in must be 16-byte aligned");
     }
     DeviceGuard g(device);
     hipStream_t st = as_stream(stream);

@@ -97,6 +97,15 @@ def test_gnorm_partials_query_and_argument_checks(native):
     with pytest.raises(ValueError, match="wgrad_splits"):
         c.wgrad_splits = 16
         native.call("dxrl_pg_fused_pair_gnorm", 0, C.byref(c), C.byref(a), 4096, 2572, C.byref(nb), None)
+    # the stored layer-2 rows move in 16-byte pieces: misaligned pointers are refused up front
+    c.rows = a.rows = 32 * 256
+    c.wgrad_splits = 128
+    a.h2_in = fake + 8
+    with pytest.raises(ValueError, match="h2_in must be 16-byte aligned"):
+        native.call("dxrl_pg_fused_pair_gnorm", 0, C.byref(c), C.byref(a), 4096, 2572, C.byref(nb), None)
+    with pytest.raises(ValueError, match="h2_in / h2_out must be 16-byte aligned"):
+        native.call("dxrl_pg_fused", 0, C.byref(a), None)
+    a.h2_in = None
     with pytest.raises(ValueError, match="padded parameter count"):
         native.call("dxrl_pg_adam_step", 0, *([fake] * 7), 12345, 3e-4, 0.9, 0.999, 1e-5, 1, 0.5, fake, 2572, fake,
                     fake, None)

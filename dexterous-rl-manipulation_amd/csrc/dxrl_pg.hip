@@ -1768,8 +1768,8 @@ int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, cons
     DeviceGuard g(env->device);
     const int64_t n = env->cfg.num_envs;
     DXRL_REQUIRE((reinterpret_cast<uintptr_t>(a->h2_tape) & 15) == 0, "pg_rollout: h2_tape must be 16-byte aligned");
-    DXRL_REQUIRE(!a->h2_tape || rollout_kernel(n, a->diag_flags, a->obs_fm != nullptr) == 1,
-                 "h2_tape is written by the 16-env rollout kernel only (dxrl_pg_rollout_kernel)");
+    DXRL_REQUIRE(!a->h2_tape || rollout_kernel(n, a->diag_flags, a->obs_fm != nullptr) != 0,
+                 "h2_tape is written by the 16- and 32-env rollout kernels only (dxrl_pg_rollout_kernel)");
     if (a->obs_fm || (a->diag_flags & 16)) {  // feature-major tape / A-B reference: the 64-env kernel
         hipLaunchKernelGGL(k_pg_rollout, dim3((unsigned)((n + kTile - 1) / kTile)), dim3(64 * kRolloutWaves), 0,
                            as_stream(stream), p);

@@ -625,6 +625,17 @@ __global__ __launch_bounds__(kE8Threads, 1) void k_pg_rollout_e8(PgRolloutArgs p
 #pragma unroll
             for (int q = 0; q < 4; ++q) MU[(16 * rt + 4 * g16 + q) * (kOut + 1) + r16] = acc[q] + b3_reg;
         }
+        if (mlp && p.h2_tape) {
+            // the step's H2 rows (32 envs x 32 chunks of 16 bytes; chunk c of row r at c ^ (r & 15))
+            // to the actor's layer-2 tape, two chunks per thread
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int q = tid + 512 * u, row = q >> 5, c = q & 31;
+                const int64_t ie = (int64_t)blockIdx.x * kE8Envs + row;
+                const bf16x8 v = *reinterpret_cast<const bf16x8*>(H2 + row * kHsW + ((c ^ (row & 15)) << 3));
+                if (ie < n) __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p.h2_tape + (t * n + ie) * kH2Ld + 8 * c));
+            }
+        }
         step_draws(ctr, t);
         E8_STAMP(3);
         lds_barrier();

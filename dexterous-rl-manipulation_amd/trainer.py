@@ -38,6 +38,8 @@ from .envs import VecEnv
 # csrc/dxrl_pg.h
 OBS_IN, IN, H, HX, OUT, ACT, ACT_PAD = 45, 64, 256, 288, 32, 15, 16
 H2LD = 264  # row pitch (bf16) of the stored layer-2 activations: the fused learner's H2 tile rows
+# rollout kernels (dxrl_pg_rollout_kernel) whose calls write the actor's layer-2 tape
+TAPE_KERNELS = (1, 2)
 W1, W2, W3 = H * IN, H * HX, OUT * HX
 OFF = {"W1a": 0, "W2a": W1, "W3a": W1 + W2, "logstd": W1 + W2 + W3}
 OFF["W1c"] = OFF["logstd"] + 32
@@ -370,12 +372,12 @@ class PGTrainer:
         a.applied_act = p(getattr(self, "applied_act", None))  # parity tapes (tests only; None in runs)
         a.dyn_noise_tape = p(getattr(self, "dyn_noise_tape", None))
         a.obs_noise_tape = p(getattr(self, "obs_noise_tape", None))
-        # the actor's H2 tape (the 16-env kernel writes it; the 32-env one has no registers left)
+        # the actor's H2 tape (written by the 16- and 32-env kernels, not the 64-env reference one)
         tape = False
         if self.cfg.fused and self.cfg.reuse_h2:
             k = C.c_int32()
             N.call("dxrl_pg_rollout_kernel", self.env.handle, self.diag_flags, C.byref(k))
-            tape = k.value == 1
+            tape = k.value in TAPE_KERNELS
             if tape and self.h2a is None:  # zero padding columns (the learner's LDS-DMA reads them)
                 self.h2a = torch.zeros(self.M, H2LD, dtype=torch.bfloat16, device=self.dev)
         a.h2_tape = p(self.h2a) if tape else None

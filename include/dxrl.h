@@ -297,9 +297,10 @@ typedef struct dxrl_pg_rollout_args {
     float* dyn_noise_tape;     /* f32 [T N][16] dynamics noise per action dim (0 if off)    */
     float* obs_noise_tape;     /* f32 [(T+1) N][48] observation noise per obs element       */
     void* h2_tape;             /* bf16 [T N][264] the actor's layer-2 activations of every step
-                                  (nullable; written by the 16-env kernel only, see
-                                  dxrl_pg_rollout_kernel; dxrl_pg_fused_args.h2_in of the actor's
-                                  first train pass under these weights)                        */
+                                  (nullable; written by the 16- and 32-env kernels, not the 64-env
+                                  reference one, see dxrl_pg_rollout_kernel;
+                                  dxrl_pg_fused_args.h2_in of the actor's first train pass under
+                                  these weights)                                               */
 } dxrl_pg_rollout_args;
 
 /* Fused policy + env rollout: T steps of actor MLP (bf16 MFMA) -> Gaussian
@@ -307,7 +308,7 @@ typedef struct dxrl_pg_rollout_args {
 int dxrl_pg_rollout(dxrl_env* env, const void* packed, const float* params, const dxrl_pg_rollout_args* args,
                     void* stream);
 /* Which kernel dxrl_pg_rollout runs for this env and diag_flags (without a feature-major tape):
- * 1 the 16-env kernel (< 32 envs per CU; the only one that writes h2_tape), 2 the 32-env kernel,
+ * 1 the 16-env kernel (< 32 envs per CU), 2 the 32-env kernel (both write h2_tape),
  * 0 the 64-env reference kernel (diag_flags & 16).  Host-only query. */
 int dxrl_pg_rollout_kernel(const dxrl_env* env, int32_t diag_flags, int32_t* kernel);
 

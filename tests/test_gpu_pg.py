@@ -216,18 +216,22 @@ def test_paired_learner_equals_two_passes(pkg, n, T, mb):
         assert torch.equal(la, lb)
 
 
-@pytest.mark.parametrize("n,T,mb,paired", [(4096, 32, 1, True), (773, 32, 1, True), (2048, 32, 4, True),
-                                          (1001, 32, 1, False), (8192, 8, 1, True), (5, 32, 1, True)])
-def test_stored_h2_equals_recomputed(pkg, n, T, mb, paired):
-    """TrainerConfig.reuse_h2: the actor's layer-2 activations written by the rollout (16-env
-    kernel) and the critic's written by the critic-values pass, read by the first train passes
-    under those weights (LDS-DMA into the H2 tile), give the recomputing passes' results bit for
-    bit: V, every minibatch's gradients, loss sums and dH2 of both networks.  Ragged tiles, PPO
-    slices, the per-network path, 8192 envs (the 32-env rollout kernel's tape), and fewer rows than
-    one tile."""
+@pytest.mark.parametrize("n,T,mb,paired,diag", [(4096, 32, 1, True, 0), (773, 32, 1, True, 0),
+                                               (2048, 32, 4, True, 0), (1001, 32, 1, False, 0),
+                                               (8192, 8, 1, True, 0), (5, 32, 1, True, 0),
+                                               (1000, 32, 1, True, 1024)])
+def test_stored_h2_equals_recomputed(pkg, n, T, mb, paired, diag):
+    """TrainerConfig.reuse_h2: the actor's layer-2 activations written by the rollout (16- and
+    32-env kernels) and the critic's written by the critic-values pass, read by the first train
+    passes under those weights (LDS-DMA into the H2 tile), give the recomputing passes' results bit
+    for bit: V, every minibatch's gradients, loss sums and dH2 of both networks.  Ragged tiles, PPO
+    slices, the per-network path, 8192 envs (the 32-env rollout kernel's tape), the 32-env kernel
+    forced on a ragged 1000 envs (diag 1024: a partial last workgroup), and fewer rows than one
+    tile."""
     outs = []
     for reuse in (True, False):
         _, tr = make(pkg, n, T, minibatches=mb, reuse_h2=reuse)
+        tr.diag_flags = diag
         if not paired:
             tr.paired = False
         tr.rollout()
